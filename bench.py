@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""bench.py — SpGEMM GFLOP/s (2*flops(A*A)/t) + output nnz/s, fp64, on N MI355X.
+
+Contract:
+  python bench.py --gpus N --steps K --warmup W
+One step = one full C = A*A of this rank's row block through the C-ABI
+two-phase entry points (ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute:
+row analysis, binning, symbolic, scan, host read of nnz, numeric + write C),
+inputs resident in HBM, C written into preallocated device arrays.
+
+Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15,
+edge factor 20, scale 20 + log2(N) — at N=1 this is the north-star headline
+matrix (1M rows, ~20 nnz/row; SURVEY.md §8 K3'), at N=8 a 8M-row matrix of the
+K4 family.  Rows are sharded by equal products (flops prefix) across ranks with
+B replicated (broadcast once over RCCL before timing); per-rank work is fixed
+as N grows, hence "scaling": "weak".  No collective inside the timed region
+(C stays sharded; the allgatherv of C is measured separately by
+tools/gather_bench.py).
+"""
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ia-spgemm_amd"))
+
+import numpy as np  # noqa: E402
+
+METRIC = "SpGEMM GFLOP/s (2·flops(A·A)/t) + output nnz/s, fp64, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+
+CONFIGS = {
+    # name: (kind, params, description)
+    "k1": ("band", dict(n=1 << 18, h=3, seed=7), "banded 256k x 256k, 7 diagonals (CSR path)"),
+    "k2": ("ell", dict(n=1 << 20, k=16, seed=7), "ELL-shaped 1M x 1M, 16 nnz/row (CSR path)"),
+    "k3": ("rmat", dict(scale=20, ef=32, seed=1), "R-MAT 2^20, avg 32 nnz/row"),
+    "k3p": ("rmat", dict(scale=20, ef=20, seed=2), "R-MAT 2^20, ~20 nnz/row (north-star headline)"),
+    "k4": ("rmat", dict(scale=23, ef=24, seed=3), "R-MAT 2^23, avg 24 nnz/row"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="auto", help="auto | " + " | ".join(CONFIGS))
+    p.add_argument("--order", default="reference", choices=["reference", "sorted"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def workload(cfg: str, world: int):
+    if cfg == "auto":
+        scale = 20 + int(round(math.log2(max(world, 1))))
+        return "rmat", dict(scale=scale, ef=20, seed=2), (
+            f"R-MAT 2^{scale}, edge factor 20, (a,b,c)=(.45,.15,.15); N=1: north-star K3'")
+    kind, prm, desc = CONFIGS[cfg]
+    return kind, dict(prm), desc
+
+
+def generate(kind, prm):
+    import ias
+    if kind == "rmat":
+        return ias.gen_rmat(prm["scale"], prm["ef"], 0.45, 0.15, 0.15, prm["seed"], 0)
+    if kind == "band":
+        return ias.gen_band(prm["n"], prm["h"], prm["seed"], 0)
+    if kind == "ell":
+        return ias.gen_ell(prm["n"], prm["k"], prm["seed"], 0)
+    raise ValueError(kind)
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world == 1:
+        world_req = args.gpus
+    else:
+        world_req = world
+    import torch
+    import torch.distributed as dist
+    import ias
+
+    dist_on = world > 1
+    if dist_on:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    kind, prm, desc = workload(args.config, world_req)
+    # ---------------- inputs: rank 0 generates, B replicated by broadcast
+    t_gen = time.time()
+    meta = torch.zeros(4, dtype=torch.int64)
+    if rank == 0:
+        A = generate(kind, prm)
+        meta[:] = torch.tensor([A.rows, A.cols, A.nnz, ias.flops(A, A)])
+        bounds = (C.c_int64 * (world + 1))()
+        sa = A.struct()
+        ias.check(ias.lib.ias_partition_rows(C.byref(sa), C.byref(sa), world, bounds), "partition")
+        bnd = torch.tensor(list(bounds), dtype=torch.int64)
+    else:
+        A = None
+        bnd = torch.zeros(world + 1, dtype=torch.int64)
+    if dist_on:
+        meta_d, bnd_d = meta.to(dev), bnd.to(dev)
+        dist.broadcast(meta_d, 0)
+        dist.broadcast(bnd_d, 0)
+        meta, bnd = meta_d.cpu(), bnd_d.cpu()
+    rows, cols, nnz_a, flops_total = [int(x) for x in meta]
+    if rank == 0:
+        rp = torch.from_numpy(A.row_ptr).to(dev)
+        ci = torch.from_numpy(A.col).to(dev)
+        va = torch.from_numpy(A.val).to(dev)
+    else:
+        rp = torch.empty(rows + 1, dtype=torch.int64, device=dev)
+        ci = torch.empty(nnz_a, dtype=torch.int32, device=dev)
+        va = torch.empty(nnz_a, dtype=torch.float64, device=dev)
+    if dist_on:
+        for t in (rp, ci, va):
+            dist.broadcast(t, 0)
+    torch.cuda.synchronize()
+    t_gen = time.time() - t_gen
+
+    def dcsr(r0, r1, rp_t, nnz):
+        return ias.Csr(r1 - r0, cols, nnz,
+                       C.cast(C.c_void_p(rp_t.data_ptr() + 8 * r0), ias.i64p),
+                       C.cast(C.c_void_p(ci.data_ptr()), ias.i32p),
+                       C.cast(C.c_void_p(va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
+
+    r0, r1 = int(bnd[rank]), int(bnd[rank + 1])
+    rp_host = rp[r0:r1 + 1].cpu()
+    Bm = dcsr(0, rows, rp, nnz_a)
+    Am = dcsr(r0, r1, rp, int(rp_host[-1] - rp_host[0]))
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
+    order = ias.ORDER_SORTED if args.order == "sorted" else ias.ORDER_REFERENCE
+
+    nnz_c = C.c_int64(0)
+    ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None, None), "nnz")
+    cap = int(nnz_c.value)
+    c_rp = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
+    c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
+    Cm = ias.Csr(r1 - r0, cols, cap, C.cast(C.c_void_p(c_rp.data_ptr()), ias.i64p),
+                 C.cast(C.c_void_p(c_ci.data_ptr()), ias.i32p),
+                 C.cast(C.c_void_p(c_va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
+    rep = ias.Report()
+
+    def step():
+        n = C.c_int64(0)
+        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None, None), "nnz")
+        Cm.nnz = cap
+        ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
+                                                  C.byref(rep)), "compute")
+        return rep
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reps = []
+    for _ in range(args.steps):
+        r = step()
+        reps.append((r.ms_total, r.ms_analysis, r.ms_symbolic, r.ms_numeric))
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    nnz_tot = torch.tensor([float(cap)], dtype=torch.float64, device=dev)
+    num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(nnz_tot, op=dist.ReduceOp.SUM)
+        dist.all_reduce(num_ms, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max.item())
+    ms_step = 1000.0 * elapsed / args.steps
+    gflops = 2.0 * flops_total / (ms_step * 1e6)
+    nnz_c_total = int(nnz_tot.item())
+
+    # roofline of the numeric phase (dominant: it writes C) on this rank
+    rows_local = r1 - r0
+    bytes_a = 8 * (rows_local + 1) + 12 * int(Am.nnz)
+    bytes_b = 8 * (rows + 1) + 12 * nnz_a
+    bytes_c = 8 * (rows_local + 1) + 12 * cap
+    alg_bytes = bytes_a + bytes_b + bytes_c
+    num_ms_local = statistics.mean(x[3] for x in reps)
+    achieved = alg_bytes / (num_ms_local * 1e-3) / 1e9
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
+    if os.path.exists(pmc_file):
+        try:
+            traffic = json.load(open(pmc_file)).get("numeric_hbm_bytes_per_step")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": round(gflops, 3),
+        "unit": "GFLOP/s",
+        "n_gpus": world_req,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (deterministic R-MAT/band/ELL generator, ia-spgemm_amd/csrc/gen.cpp)",
+        "config": {
+            "workload": desc,
+            "kind": kind, **prm,
+            "rows": rows, "nnz_a": nnz_a, "flops": flops_total, "nnz_c": nnz_c_total,
+            "order": args.order,
+            "parallelism": f"row-block x{world_req}, B replicated",
+        },
+        "nnz_per_s": round(nnz_c_total / (ms_step * 1e-3), 1),
+        "phases_ms_rank0": {
+            "total_device": round(statistics.mean(x[0] for x in reps), 4),
+            "analysis": round(statistics.mean(x[1] for x in reps), 4),
+            "symbolic": round(statistics.mean(x[2] for x in reps), 4),
+            "numeric": round(statistics.mean(x[3] for x in reps), 4),
+        },
+        "roofline": {
+            "kernel": "numeric phase (k_numeric_lds<*> + k_numeric_global bins)",
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "alg_bytes": alg_bytes,
+        },
+        "setup_s": round(t_gen, 2),
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind in ("rmat", "band", "ell"):
+        out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
+        if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
+            out["speedup_vs_cpu_baseline"] = round(gflops / out["cpu_baseline"]["value"], 2)
+
+    ias.lib.ias_plan_destroy(plan)
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(A, flops_total, threads):
+    """The reference's Algorithm 1 (MKL mkl_sparse_sp2m, create+multiply+export
+    as main.cpp:746-748) on the host cores: 1 warm-up + median of 3 full runs."""
+    import ias
+    ok, ver = ias.mkl_available()
+    if not ok:
+        return {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "reference",
+                "sample": "MKL runtime not present on this host"}
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    times = []
+    sa = A.struct()
+    for i in range(4):
+        cm, ms = ias.Csr(), C.c_double(0)
+        ias.check(ias.lib.ias_mkl_sp2m(C.byref(sa), C.byref(sa), C.byref(cm), threads, C.byref(ms)),
+                  "ias_mkl_sp2m")
+        ias.lib.ias_csr_free(C.byref(cm))
+        if i:
+            times.append(ms.value)
+    med = statistics.median(times)
+    return {"value": round(2.0 * flops_total / (med * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"full matrix, MKL mkl_sparse_sp2m FULL_MULT (reference Algorithm 1, "
+                      f"csr/common_csr.h:18-47), {ver.split(' Product')[0]}, LP64, GNU threading, "
+                      f"median of 3 after 1 warm-up: {med:.1f} ms",
+            "ms": round(med, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,647 @@
+// ias_api.hip — C-ABI glue of libias.so: memory, plans, the SpGEMM entry
+// points (CSR / COO / ELL over the shared engine), two-phase form, sums,
+// flops, row views and multi-GPU helpers.  Reference counterparts are cited
+// per function in include/ias.h.
+#include "ias.h"
+#include "ias_internal.hpp"
+#include "spgemm_engine.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <memory>
+#include <vector>
+
+namespace ias {
+
+static thread_local char g_last_error[512] = "";
+
+void set_last_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_last_error, sizeof g_last_error, fmt, ap);
+    va_end(ap);
+}
+
+void *host_alloc(size_t bytes, bool zero) {
+    void *p = zero ? calloc(bytes ? bytes : 1, 1) : malloc(bytes ? bytes : 1);
+    return p;
+}
+void host_free(void *p) { free(p); }
+
+#define HIPC(x)                                                                   \
+    do {                                                                          \
+        hipError_t _e = (x);                                                      \
+        if (_e != hipSuccess) {                                                   \
+            set_last_error("%s failed: %s", #x, hipGetErrorString(_e));           \
+            return _e == hipErrorOutOfMemory ? IAS_ERROR_OUT_OF_MEMORY : IAS_ERROR_DEVICE; \
+        }                                                                         \
+    } while (0)
+
+ias_status dev_alloc(void **p, size_t bytes, int device) {
+    *p = nullptr;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMalloc(p, bytes ? bytes : 8));
+    return IAS_SUCCESS;
+}
+ias_status dev_free(void *p, int device) {
+    if (!p) return IAS_SUCCESS;
+    HIPC(hipSetDevice(device));
+    HIPC(hipFree(p));
+    return IAS_SUCCESS;
+}
+ias_status dev_copy_h2d(void *dst, const void *src, size_t bytes, int device) {
+    if (!bytes) return IAS_SUCCESS;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return IAS_SUCCESS;
+}
+ias_status dev_copy_d2h(void *dst, const void *src, size_t bytes, int device) {
+    if (!bytes) return IAS_SUCCESS;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return IAS_SUCCESS;
+}
+ias_status dev_memset(void *p, int value, size_t bytes, int device) {
+    if (!bytes) return IAS_SUCCESS;
+    HIPC(hipSetDevice(device));
+    HIPC(hipMemset(p, value, bytes));
+    return IAS_SUCCESS;
+}
+
+ias_status check_csr_host(const ias_csr *A) {
+    if (A->rows < 0 || A->cols < 0 || A->nnz < 0) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->rows > INT32_MAX || A->cols > INT32_MAX) return IAS_ERROR_OVERFLOW;
+    if (!A->row_ptr) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->nnz > 0 && (!A->col || !A->val)) return IAS_ERROR_INVALID_ARGUMENT;
+    return IAS_SUCCESS;
+}
+
+// Generic copy of one array between host/device memories.
+static ias_status move_bytes(void **dst, const void *src, size_t bytes, int src_mem, int src_dev,
+                             int dst_mem, int dst_dev) {
+    *dst = nullptr;
+    if (dst_mem == IAS_MEMORY_DEVICE) {
+        IAS_TRY(dev_alloc(dst, bytes, dst_dev));
+        if (!bytes || !src) return IAS_SUCCESS;
+        HIPC(hipSetDevice(dst_dev));
+        if (src_mem == IAS_MEMORY_DEVICE) HIPC(hipMemcpy(*dst, src, bytes, hipMemcpyDeviceToDevice));
+        else HIPC(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+    } else {
+        *dst = host_alloc(bytes, false);
+        if (!*dst) return IAS_ERROR_OUT_OF_MEMORY;
+        if (!bytes || !src) return IAS_SUCCESS;
+        if (src_mem == IAS_MEMORY_DEVICE) {
+            HIPC(hipSetDevice(src_dev));
+            HIPC(hipMemcpy(*dst, src, bytes, hipMemcpyDeviceToHost));
+        } else {
+            memcpy(*dst, src, bytes);
+        }
+    }
+    return IAS_SUCCESS;
+}
+
+static void release(void *p, int mem, int dev) {
+    if (!p) return;
+    if (mem == IAS_MEMORY_DEVICE) dev_free(p, dev);
+    else free(p);
+}
+
+}  // namespace ias
+
+using namespace ias;
+
+// =================================================================== misc
+extern "C" int ias_abi_version(void) { return IAS_ABI_VERSION; }
+
+extern "C" const char *ias_status_string(ias_status s) {
+    switch (s) {
+        case IAS_SUCCESS: return "success";
+        case IAS_ERROR_INVALID_ARGUMENT: return "invalid argument";
+        case IAS_ERROR_DIMENSION_MISMATCH: return "dimension mismatch";
+        case IAS_ERROR_OUT_OF_MEMORY: return "out of memory";
+        case IAS_ERROR_DEVICE: return "device error";
+        case IAS_ERROR_IO: return "I/O error";
+        case IAS_ERROR_FORMAT: return "bad Matrix-Market format";
+        case IAS_ERROR_UNSUPPORTED: return "unsupported";
+        case IAS_ERROR_INFEASIBLE: return "format infeasible under the size gate";
+        case IAS_ERROR_OVERFLOW: return "index overflow";
+        case IAS_ERROR_UNAVAILABLE: return "runtime unavailable";
+        case IAS_ERROR_INSUFFICIENT_CAPACITY: return "insufficient capacity";
+    }
+    return "unknown status";
+}
+
+extern "C" const char *ias_last_error(void) { return g_last_error; }
+
+extern "C" ias_status ias_device_count(int32_t *count) {
+    if (!count) return IAS_ERROR_INVALID_ARGUMENT;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        set_last_error("hipGetDeviceCount: %s", hipGetErrorString(e));
+        return IAS_ERROR_DEVICE;
+    }
+    *count = n;
+    return IAS_SUCCESS;
+}
+
+extern "C" void ias_opts_default(ias_opts *o) {
+    if (!o) return;
+    memset(o, 0, sizeof *o);
+    o->order = IAS_ORDER_REFERENCE;
+    o->output_memory = -1;
+    o->device = -1;
+}
+
+extern "C" ias_status ias_plan_create(ias_plan **plan, int32_t device, void *stream) {
+    if (!plan) return IAS_ERROR_INVALID_ARGUMENT;
+    *plan = nullptr;
+    int32_t n = 0;
+    IAS_TRY(ias_device_count(&n));
+    if (device < 0 || device >= n) {
+        set_last_error("device %d not present (%d devices)", device, n);
+        return IAS_ERROR_DEVICE;
+    }
+    std::unique_ptr<ias_plan> p(new ias_plan());
+    IAS_TRY(p->init(device, stream));
+    *plan = p.release();
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_plan_destroy(ias_plan *plan) {
+    delete plan;
+    return IAS_SUCCESS;
+}
+
+// =================================================================== memory
+extern "C" ias_status ias_csr_alloc(ias_csr *m, int64_t rows, int64_t cols, int64_t nnz,
+                                    int32_t memory, int32_t device) {
+    if (!m || rows < 0 || cols < 0 || nnz < 0) return IAS_ERROR_INVALID_ARGUMENT;
+    memset(m, 0, sizeof *m);
+    m->rows = rows; m->cols = cols; m->nnz = nnz; m->memory = memory; m->device = device;
+    void *a = nullptr, *b = nullptr, *c = nullptr;
+    ias_status s;
+    if ((s = move_bytes(&a, nullptr, sizeof(int64_t) * (rows + 1), memory, device, memory, device)) ||
+        (s = move_bytes(&b, nullptr, sizeof(int32_t) * nnz, memory, device, memory, device)) ||
+        (s = move_bytes(&c, nullptr, sizeof(double) * nnz, memory, device, memory, device))) {
+        release(a, memory, device); release(b, memory, device); release(c, memory, device);
+        memset(m, 0, sizeof *m);
+        return s;
+    }
+    m->row_ptr = (int64_t *)a; m->col = (int32_t *)b; m->val = (double *)c;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_csr_copy(const ias_csr *src, ias_csr *dst, int32_t memory,
+                                   int32_t device) {
+    if (!src || !dst) return IAS_ERROR_INVALID_ARGUMENT;
+    ias_csr t{};
+    t.rows = src->rows; t.cols = src->cols; t.nnz = src->nnz; t.memory = memory; t.device = device;
+    void *a = nullptr, *b = nullptr, *c = nullptr;
+    ias_status s;
+    if ((s = move_bytes(&a, src->row_ptr, sizeof(int64_t) * (src->rows + 1), src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&b, src->col, sizeof(int32_t) * src->nnz, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&c, src->val, sizeof(double) * src->nnz, src->memory, src->device, memory, device))) {
+        release(a, memory, device); release(b, memory, device); release(c, memory, device);
+        return s;
+    }
+    t.row_ptr = (int64_t *)a; t.col = (int32_t *)b; t.val = (double *)c;
+    *dst = t;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_csr_free(ias_csr *m) {
+    if (!m) return IAS_ERROR_INVALID_ARGUMENT;
+    release(m->row_ptr, m->memory, m->device);
+    release(m->col, m->memory, m->device);
+    release(m->val, m->memory, m->device);
+    memset(m, 0, sizeof *m);
+    return IAS_SUCCESS;
+}
+extern "C" ias_status ias_coo_free(ias_coo *m) {
+    if (!m) return IAS_ERROR_INVALID_ARGUMENT;
+    release(m->row_offset, m->memory, m->device);
+    release(m->row, m->memory, m->device);
+    release(m->col, m->memory, m->device);
+    release(m->val, m->memory, m->device);
+    memset(m, 0, sizeof *m);
+    return IAS_SUCCESS;
+}
+extern "C" ias_status ias_ell_free(ias_ell *m) {
+    if (!m) return IAS_ERROR_INVALID_ARGUMENT;
+    release(m->nnz_row, m->memory, m->device);
+    release(m->col, m->memory, m->device);
+    release(m->val, m->memory, m->device);
+    memset(m, 0, sizeof *m);
+    return IAS_SUCCESS;
+}
+extern "C" ias_status ias_dia_free(ias_dia *m) {
+    if (!m) return IAS_ERROR_INVALID_ARGUMENT;
+    release(m->diagonal_offsets, m->memory, m->device);
+    release(m->diagonal_ind, m->memory, m->device);
+    release(m->val, m->memory, m->device);
+    memset(m, 0, sizeof *m);
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_coo_copy(const ias_coo *src, ias_coo *dst, int32_t memory, int32_t device) {
+    if (!src || !dst) return IAS_ERROR_INVALID_ARGUMENT;
+    ias_coo t = *src;
+    t.memory = memory; t.device = device;
+    void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+    ias_status s;
+    if ((s = move_bytes(&a, src->row_offset, sizeof(int64_t) * (src->rows + 1), src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&b, src->row, sizeof(int32_t) * src->nnz, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&c, src->col, sizeof(int32_t) * src->nnz, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&d, src->val, sizeof(double) * src->nnz, src->memory, src->device, memory, device))) {
+        release(a, memory, device); release(b, memory, device); release(c, memory, device); release(d, memory, device);
+        return s;
+    }
+    t.row_offset = (int64_t *)a; t.row = (int32_t *)b; t.col = (int32_t *)c; t.val = (double *)d;
+    *dst = t;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_ell_copy(const ias_ell *src, ias_ell *dst, int32_t memory, int32_t device) {
+    if (!src || !dst) return IAS_ERROR_INVALID_ARGUMENT;
+    ias_ell t = *src;
+    t.memory = memory; t.device = device;
+    const size_t rk = (size_t)src->rows * (size_t)src->max_nnz_per_row;
+    void *a = nullptr, *b = nullptr, *c = nullptr;
+    ias_status s;
+    if ((s = move_bytes(&a, src->nnz_row, sizeof(int32_t) * src->rows, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&b, src->col, sizeof(int32_t) * rk, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&c, src->val, sizeof(double) * rk, src->memory, src->device, memory, device))) {
+        release(a, memory, device); release(b, memory, device); release(c, memory, device);
+        return s;
+    }
+    t.nnz_row = (int32_t *)a; t.col = (int32_t *)b; t.val = (double *)c;
+    *dst = t;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_dia_copy(const ias_dia *src, ias_dia *dst, int32_t memory, int32_t device) {
+    if (!src || !dst) return IAS_ERROR_INVALID_ARGUMENT;
+    ias_dia t = *src;
+    t.memory = memory; t.device = device;
+    const size_t rn = (size_t)src->rows * (size_t)src->num_diagonals;
+    const size_t span = (size_t)std::max<int64_t>(src->rows + src->cols - 1, 0);
+    void *a = nullptr, *b = nullptr, *c = nullptr;
+    ias_status s;
+    if ((s = move_bytes(&a, src->diagonal_offsets, sizeof(int32_t) * src->num_diagonals, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&b, src->diagonal_ind, sizeof(int32_t) * span, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&c, src->val, sizeof(double) * rn, src->memory, src->device, memory, device))) {
+        release(a, memory, device); release(b, memory, device); release(c, memory, device);
+        return s;
+    }
+    t.diagonal_offsets = (int32_t *)a; t.diagonal_ind = (int32_t *)b; t.val = (double *)c;
+    *dst = t;
+    return IAS_SUCCESS;
+}
+
+// =================================================================== SpGEMM
+namespace {
+
+// A temporary plan when the caller did not pass one.
+struct PlanGuard {
+    ias_plan *p = nullptr;
+    bool owned = false;
+    ~PlanGuard() {
+        if (owned) ias_plan_destroy(p);
+    }
+    ias_status acquire(const ias_opts &o, int device) {
+        if (o.plan) {
+            p = o.plan;
+            return IAS_SUCCESS;
+        }
+        owned = true;
+        return ias_plan_create(&p, device, o.stream);
+    }
+};
+
+// Device-resident copies of host operands, released at scope exit.
+struct Staged {
+    std::vector<std::pair<void *, int>> owned;
+    ~Staged() {
+        for (auto &x : owned) dev_free(x.first, x.second);
+    }
+    template <typename T>
+    ias_status stage(const T *src, size_t count, int mem, int srcdev, int device, const T **out) {
+        if (mem == IAS_MEMORY_DEVICE && srcdev == device) {
+            *out = src;
+            return IAS_SUCCESS;
+        }
+        void *d = nullptr;
+        IAS_TRY(move_bytes(&d, src, sizeof(T) * count, mem, srcdev, IAS_MEMORY_DEVICE, device));
+        owned.push_back({d, device});
+        *out = (const T *)d;
+        return IAS_SUCCESS;
+    }
+};
+
+ias_opts resolve(const ias_opts *opts) {
+    ias_opts o;
+    ias_opts_default(&o);
+    if (opts) o = *opts;
+    return o;
+}
+
+int pick_device(const ias_opts &o, int a_mem, int a_dev) {
+    if (o.device >= 0) return o.device;
+    if (a_mem == IAS_MEMORY_DEVICE) return a_dev;
+    return 0;
+}
+
+double ms_since(hipEvent_t a, hipEvent_t b) {
+    float t = 0;
+    hipEventElapsedTime(&t, a, b);
+    return t;
+}
+
+}  // namespace
+
+extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_csr *C,
+                                      const ias_opts *opts, ias_report *rep) {
+    if (!A || !B || !C) return IAS_ERROR_INVALID_ARGUMENT;
+    IAS_TRY(check_csr_host(A));
+    IAS_TRY(check_csr_host(B));
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    const ias_opts o = resolve(opts);
+    if (o.order != IAS_ORDER_REFERENCE && o.order != IAS_ORDER_SORTED) return IAS_ERROR_INVALID_ARGUMENT;
+    const int device = pick_device(o, A->memory, A->device);
+    const int out_mem = o.output_memory >= 0 ? o.output_memory : A->memory;
+    if (rep) memset(rep, 0, sizeof *rep);
+    PlanGuard pg;
+    IAS_TRY(pg.acquire(o, device));
+    ias_plan *plan = pg.p;
+    HIPC(hipSetDevice(plan->device));
+    hipStream_t s = (hipStream_t)plan->stream;
+
+    Staged st;
+    const int64_t *ap, *bp;
+    const int32_t *ac, *bc;
+    const double *av, *bv;
+    HIPC(hipEventRecord(plan->ev[5], s));
+    IAS_TRY(st.stage(A->row_ptr, A->rows + 1, A->memory, A->device, plan->device, &ap));
+    IAS_TRY(st.stage(A->col, A->nnz, A->memory, A->device, plan->device, &ac));
+    IAS_TRY(st.stage(A->val, A->nnz, A->memory, A->device, plan->device, &av));
+    if (B == A) {
+        bp = ap; bc = ac; bv = av;
+    } else {
+        IAS_TRY(st.stage(B->row_ptr, B->rows + 1, B->memory, B->device, plan->device, &bp));
+        IAS_TRY(st.stage(B->col, B->nnz, B->memory, B->device, plan->device, &bc));
+        IAS_TRY(st.stage(B->val, B->nnz, B->memory, B->device, plan->device, &bv));
+    }
+    dev::Rows ra{ap, nullptr, 0, ac, av};
+    dev::Rows rb{bp, nullptr, 0, bc, bv};
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    const int64_t nnz = plan->nnz_total;
+
+    ias_csr D{};
+    IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
+    HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                        hipMemcpyDeviceToDevice, s));
+    dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0};
+    ias_status stn = plan->numeric(ra, rb, out, rep);
+    if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
+        stn = ias_sort_rows_device(plan, D.row_ptr, A->rows, D.col, D.val, plan->max_nnz);
+    if (stn != IAS_SUCCESS) {
+        ias_csr_free(&D);
+        return stn;
+    }
+    HIPC(hipStreamSynchronize(s));
+    if (out_mem == IAS_MEMORY_HOST) {
+        ias_csr H{};
+        ias_status cs = ias_csr_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        ias_csr_free(&D);
+        if (cs != IAS_SUCCESS) return cs;
+        *C = H;
+    } else {
+        *C = D;
+    }
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_coo *C,
+                                      const ias_opts *opts, ias_report *rep) {
+    if (!A || !B || !C) return IAS_ERROR_INVALID_ARGUMENT;
+    if (!A->choice || !B->choice) return IAS_ERROR_INFEASIBLE;
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    const ias_opts o = resolve(opts);
+    const int device = pick_device(o, A->memory, A->device);
+    const int out_mem = o.output_memory >= 0 ? o.output_memory : A->memory;
+    if (rep) memset(rep, 0, sizeof *rep);
+    PlanGuard pg;
+    IAS_TRY(pg.acquire(o, device));
+    ias_plan *plan = pg.p;
+    HIPC(hipSetDevice(plan->device));
+    hipStream_t s = (hipStream_t)plan->stream;
+    Staged st;
+    const int64_t *ap, *bp;
+    const int32_t *ac, *bc;
+    const double *av, *bv;
+    IAS_TRY(st.stage(A->row_offset, A->rows + 1, A->memory, A->device, plan->device, &ap));
+    IAS_TRY(st.stage(A->col, A->nnz, A->memory, A->device, plan->device, &ac));
+    IAS_TRY(st.stage(A->val, A->nnz, A->memory, A->device, plan->device, &av));
+    if (B == A) {
+        bp = ap; bc = ac; bv = av;
+    } else {
+        IAS_TRY(st.stage(B->row_offset, B->rows + 1, B->memory, B->device, plan->device, &bp));
+        IAS_TRY(st.stage(B->col, B->nnz, B->memory, B->device, plan->device, &bc));
+        IAS_TRY(st.stage(B->val, B->nnz, B->memory, B->device, plan->device, &bv));
+    }
+    dev::Rows ra{ap, nullptr, 0, ac, av};
+    dev::Rows rb{bp, nullptr, 0, bc, bv};
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    const int64_t nnz = plan->nnz_total;
+    ias_coo D{};
+    D.rows = A->rows; D.cols = B->cols; D.nnz = nnz; D.memory = IAS_MEMORY_DEVICE;
+    D.device = plan->device; D.choice = 1;
+    void *p0 = nullptr, *p1 = nullptr, *p2 = nullptr, *p3 = nullptr;
+    IAS_TRY(dev_alloc(&p0, sizeof(int64_t) * (A->rows + 1), plan->device));
+    D.row_offset = (int64_t *)p0;
+    ias_status sa;
+    if ((sa = dev_alloc(&p1, sizeof(int32_t) * nnz, plan->device)) ||
+        (sa = dev_alloc(&p2, sizeof(int32_t) * nnz, plan->device)) ||
+        (sa = dev_alloc(&p3, sizeof(double) * nnz, plan->device))) {
+        D.row = (int32_t *)p1; D.col = (int32_t *)p2; D.val = (double *)p3;
+        ias_coo_free(&D);
+        return sa;
+    }
+    D.row = (int32_t *)p1; D.col = (int32_t *)p2; D.val = (double *)p3;
+    HIPC(hipMemcpyAsync(D.row_offset, plan->bufs[ias_plan::B_PTR].p,
+                        sizeof(int64_t) * (A->rows + 1), hipMemcpyDeviceToDevice, s));
+    dev::Out out{D.row_offset, 0, D.col, D.val, D.row, o.order == IAS_ORDER_SORTED ? 0 : 1, 1};
+    ias_status stn = plan->numeric(ra, rb, out, rep);
+    if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
+        stn = ias_sort_rows_device(plan, D.row_offset, A->rows, D.col, D.val, plan->max_nnz);
+    if (stn != IAS_SUCCESS) {
+        ias_coo_free(&D);
+        return stn;
+    }
+    HIPC(hipStreamSynchronize(s));
+    if (out_mem == IAS_MEMORY_HOST) {
+        ias_coo H{};
+        ias_status cs = ias_coo_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        ias_coo_free(&D);
+        if (cs != IAS_SUCCESS) return cs;
+        *C = H;
+    } else {
+        *C = D;
+    }
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_ell *C,
+                                      const ias_opts *opts, ias_report *rep) {
+    if (!A || !B || !C) return IAS_ERROR_INVALID_ARGUMENT;
+    if (!A->choice || !B->choice) return IAS_ERROR_INFEASIBLE;
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    const ias_opts o = resolve(opts);
+    const int device = pick_device(o, A->memory, A->device);
+    const int out_mem = o.output_memory >= 0 ? o.output_memory : A->memory;
+    if (rep) memset(rep, 0, sizeof *rep);
+    PlanGuard pg;
+    IAS_TRY(pg.acquire(o, device));
+    ias_plan *plan = pg.p;
+    HIPC(hipSetDevice(plan->device));
+    hipStream_t s = (hipStream_t)plan->stream;
+    Staged st;
+    const int32_t *an, *bn, *ac, *bc;
+    const double *av, *bv;
+    const size_t ak = (size_t)A->rows * A->max_nnz_per_row, bk = (size_t)B->rows * B->max_nnz_per_row;
+    IAS_TRY(st.stage(A->nnz_row, A->rows, A->memory, A->device, plan->device, &an));
+    IAS_TRY(st.stage(A->col, ak, A->memory, A->device, plan->device, &ac));
+    IAS_TRY(st.stage(A->val, ak, A->memory, A->device, plan->device, &av));
+    if (B == A) {
+        bn = an; bc = ac; bv = av;
+    } else {
+        IAS_TRY(st.stage(B->nnz_row, B->rows, B->memory, B->device, plan->device, &bn));
+        IAS_TRY(st.stage(B->col, bk, B->memory, B->device, plan->device, &bc));
+        IAS_TRY(st.stage(B->val, bk, B->memory, B->device, plan->device, &bv));
+    }
+    dev::Rows ra{nullptr, an, A->max_nnz_per_row, ac, av};
+    dev::Rows rb{nullptr, bn, B->max_nnz_per_row, bc, bv};
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    const int32_t K = plan->max_nnz;
+    ias_ell D{};
+    D.rows = A->rows; D.cols = B->cols; D.nnz = plan->nnz_total; D.max_nnz_per_row = K;
+    D.choice = 1; D.memory = IAS_MEMORY_DEVICE; D.device = plan->device;
+    const size_t ck = (size_t)A->rows * (size_t)K;
+    void *p0 = nullptr, *p1 = nullptr, *p2 = nullptr;
+    ias_status sa;
+    if ((sa = dev_alloc(&p0, sizeof(int32_t) * A->rows, plan->device)) ||
+        (sa = dev_alloc(&p1, sizeof(int32_t) * ck, plan->device)) ||
+        (sa = dev_alloc(&p2, sizeof(double) * ck, plan->device))) {
+        D.nnz_row = (int32_t *)p0; D.col = (int32_t *)p1; D.val = (double *)p2;
+        ias_ell_free(&D);
+        return sa;
+    }
+    D.nnz_row = (int32_t *)p0; D.col = (int32_t *)p1; D.val = (double *)p2;
+    HIPC(hipMemcpyAsync(D.nnz_row, plan->bufs[ias_plan::B_NNZ].p, sizeof(int32_t) * A->rows,
+                        hipMemcpyDeviceToDevice, s));
+    HIPC(hipMemsetAsync(D.col, 0, sizeof(int32_t) * ck, s));
+    HIPC(hipMemsetAsync(D.val, 0, sizeof(double) * ck, s));
+    dev::Out out{nullptr, K, D.col, D.val, nullptr, 0, 0};
+    ias_status stn = plan->numeric(ra, rb, out, rep);
+    if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
+        stn = ias_sort_rows_ell_device(plan, D.nnz_row, A->rows, K, D.col, D.val);
+    if (stn != IAS_SUCCESS) {
+        ias_ell_free(&D);
+        return stn;
+    }
+    HIPC(hipStreamSynchronize(s));
+    if (out_mem == IAS_MEMORY_HOST) {
+        ias_ell H{};
+        ias_status cs = ias_ell_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        ias_ell_free(&D);
+        if (cs != IAS_SUCCESS) return cs;
+        *C = H;
+    } else {
+        *C = D;
+    }
+    return IAS_SUCCESS;
+}
+
+// ------------------------------------------------------------------- two-phase
+static ias_status check_dev_csr(const ias_csr *A, const ias_plan *plan) {
+    if (!A) return IAS_ERROR_INVALID_ARGUMENT;
+    IAS_TRY(check_csr_host(A));
+    if (A->memory != IAS_MEMORY_DEVICE || A->device != plan->device) return IAS_ERROR_INVALID_ARGUMENT;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, const ias_csr *B,
+                                          int64_t *nnz_c, int64_t *row_ptr_c, ias_report *rep) {
+    if (!plan || !nnz_c) return IAS_ERROR_INVALID_ARGUMENT;
+    IAS_TRY(check_dev_csr(A, plan));
+    IAS_TRY(check_dev_csr(B, plan));
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    if (rep) memset(rep, 0, sizeof *rep);
+    dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
+    dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    plan->last_a = A->col;
+    plan->last_b = B->col;
+    *nnz_c = plan->nnz_total;
+    if (row_ptr_c) {
+        HIPC(hipMemcpyAsync(row_ptr_c, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                            hipMemcpyDeviceToDevice, (hipStream_t)plan->stream));
+    }
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_csr *B,
+                                              ias_csr *C, int32_t order, ias_report *rep) {
+    if (!plan || !C) return IAS_ERROR_INVALID_ARGUMENT;
+    IAS_TRY(check_dev_csr(A, plan));
+    IAS_TRY(check_dev_csr(B, plan));
+    if (plan->last_a != A->col || plan->last_b != B->col || plan->n_rows != A->rows)
+        return IAS_ERROR_INVALID_ARGUMENT;
+    if (C->memory != IAS_MEMORY_DEVICE || C->device != plan->device || !C->row_ptr ||
+        (plan->nnz_total > 0 && (!C->col || !C->val)))
+        return IAS_ERROR_INVALID_ARGUMENT;
+    if (C->nnz < plan->nnz_total) return IAS_ERROR_INSUFFICIENT_CAPACITY;
+    hipStream_t s = (hipStream_t)plan->stream;
+    HIPC(hipSetDevice(plan->device));
+    HIPC(hipMemcpyAsync(C->row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                        hipMemcpyDeviceToDevice, s));
+    C->rows = A->rows;
+    C->cols = B->cols;
+    C->nnz = plan->nnz_total;
+    dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
+    dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
+    dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0};
+    IAS_TRY(plan->numeric(ra, rb, out, rep));
+    if (order == IAS_ORDER_SORTED)
+        IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, plan->max_nnz));
+    return IAS_SUCCESS;
+}
+
+// =================================================================== helpers
+extern "C" ias_status ias_csr_row_view(const ias_csr *A, int64_t r0, int64_t r1, ias_csr *view) {
+    if (!A || !view || r0 < 0 || r1 < r0 || r1 > A->rows) return IAS_ERROR_INVALID_ARGUMENT;
+    ias_csr v = *A;
+    v.rows = r1 - r0;
+    v.row_ptr = A->row_ptr + r0;
+    if (A->memory == IAS_MEMORY_HOST) {
+        v.nnz = A->row_ptr[r1] - A->row_ptr[r0];
+    } else {
+        int64_t e[2];
+        IAS_TRY(dev_copy_d2h(&e[0], A->row_ptr + r0, sizeof(int64_t), A->device));
+        IAS_TRY(dev_copy_d2h(&e[1], A->row_ptr + r1, sizeof(int64_t), A->device));
+        v.nnz = e[1] - e[0];
+    }
+    *view = v;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_row_ptr_shift(int64_t *row_ptr, int64_t count, int64_t offset,
+                                        int32_t device, void *stream) {
+    if (!row_ptr || count < 0) return IAS_ERROR_INVALID_ARGUMENT;
+    HIPC(hipSetDevice(device));
+    return ias_shift_device(row_ptr, count, offset, stream);
+}

@@ -1,0 +1,48 @@
+// ias_internal.hpp — shared host-side helpers of libias.so (not part of the ABI).
+#pragma once
+
+#include "ias.h"
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+namespace ias {
+
+// Host allocation that never returns NULL for a zero-sized request.
+void *host_alloc(size_t bytes, bool zero = true);
+void host_free(void *p);
+
+// Device helpers (defined in ias_device.hip; all return an ias_status).
+ias_status dev_alloc(void **p, size_t bytes, int device);
+ias_status dev_free(void *p, int device);
+ias_status dev_copy_h2d(void *dst, const void *src, size_t bytes, int device);
+ias_status dev_copy_d2h(void *dst, const void *src, size_t bytes, int device);
+ias_status dev_memset(void *p, int value, size_t bytes, int device);
+
+// Record the last HIP/internal error message for ias_status_string's detail.
+void set_last_error(const char *fmt, ...);
+
+inline bool is_device(int32_t memory) { return memory == IAS_MEMORY_DEVICE; }
+
+// Shape/pointer sanity of a CSR operand (no element scan).
+ias_status check_csr_host(const ias_csr *A);
+
+// Device-side row utilities used by the entry points (sort_rows.hip).
+// Sort every row of a device CSR (ptr) by column, values following.
+ias_status ias_sort_rows_device(ias_plan *plan, const int64_t *ptr, int64_t rows, int32_t *col,
+                                double *val, int32_t max_nnz);
+// Same for a device ELL (row i at i*K, nnz_row[i] entries).
+ias_status ias_sort_rows_ell_device(ias_plan *plan, const int32_t *nnz_row, int64_t rows,
+                                    int32_t K, int32_t *col, double *val);
+ias_status ias_shift_device(int64_t *p, int64_t n, int64_t off, void *stream);
+
+}  // namespace ias
+
+#define IAS_TRY(expr)                                   \
+    do {                                                \
+        ias_status _s = (expr);                         \
+        if (_s != IAS_SUCCESS) return _s;               \
+    } while (0)

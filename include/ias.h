@@ -1,0 +1,280 @@
+/*
+ * ias.h — C-ABI of the MI355X-native IA-SpGEMM engine (libias.so).
+ *
+ * This is the drop-in boundary for the reference's row-wise SpGEMM path.
+ * The reference (hipdac-lab/IA-SpGEMM) has no library: its "operator API" is a
+ * set of header-only free functions over POD structs called from main().  Every
+ * entry point below names the reference function it replaces (file:line, paths
+ * relative to IA-SPGEMM-CPU_release/ unless prefixed GPU/).
+ *
+ * Conventions:
+ *   - plain pointers and sizes, no torch / HIP types in any signature
+ *     (streams are passed as `void*` holding a hipStream_t);
+ *   - int64 row pointers and counts everywhere (the reference's `int` overflows
+ *     at nnz(C) > 2^31, format.h:36-38); int32 column indices; fp64 values;
+ *   - outputs are library-allocated, caller frees with ias_*_free()
+ *     (reference: callee mallocs C, caller calls FreeXMatrix);
+ *   - every entry point returns an ias_status instead of exit()/ignored MKL
+ *     statuses (reference: GPU/detail/common.h:62-77 exits);
+ *   - no hidden global state: everything per-call lives in an ias_plan, so the
+ *     library is reentrant per stream.
+ *   - a matrix lives either on the host or on one HIP device (`memory`,
+ *     `device`); compute entry points accept both and return C where
+ *     opts->output_memory says.
+ */
+#ifndef IAS_H
+#define IAS_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IAS_ABI_VERSION 1
+
+typedef enum ias_status {
+    IAS_SUCCESS = 0,
+    IAS_ERROR_INVALID_ARGUMENT = 1,
+    IAS_ERROR_DIMENSION_MISMATCH = 2,
+    IAS_ERROR_OUT_OF_MEMORY = 3,
+    IAS_ERROR_DEVICE = 4,          /* HIP runtime error or no device */
+    IAS_ERROR_IO = 5,              /* fopen / short read */
+    IAS_ERROR_FORMAT = 6,          /* bad Matrix-Market banner / size line */
+    IAS_ERROR_UNSUPPORTED = 7,     /* complex or dense-array .mtx, ... */
+    IAS_ERROR_INFEASIBLE = 8,      /* format gate said `choice = false` */
+    IAS_ERROR_OVERFLOW = 9,        /* an index does not fit its type */
+    IAS_ERROR_UNAVAILABLE = 10,    /* optional runtime (MKL) not present */
+    IAS_ERROR_INSUFFICIENT_CAPACITY = 11 /* caller-provided C too small */
+} ias_status;
+
+typedef enum ias_memory { IAS_MEMORY_HOST = 0, IAS_MEMORY_DEVICE = 1 } ias_memory;
+
+/* Output column order inside each row of C. */
+typedef enum ias_order {
+    /* The order the reference kernel of that format emits, value-for-value:
+     * CSR and ELL: reverse first-touch (CSR_MUL_CSR linked-list head insertion,
+     * csr/common_csr.h:164-187; ELL_MUL_ELL ell/common_ell.h:163-185);
+     * COO: forward first-touch (COO_MUL_COO linear probe, coo/common_coo.h:136-156).
+     * Values are summed in the reference's product order without FMA
+     * contraction, so integer and fp64 results are bit-identical to it. */
+    IAS_ORDER_REFERENCE = 0,
+    /* Ascending column index inside each row (MKL/cuSPARSE-like canonical). */
+    IAS_ORDER_SORTED = 1
+} ias_order;
+
+/* CsrMatrix (detail/format.h:31-41). */
+typedef struct ias_csr {
+    int64_t rows, cols, nnz;
+    int64_t *row_ptr;   /* rows+1 entries; row i is [row_ptr[i], row_ptr[i+1]) */
+    int32_t *col;       /* nnz */
+    double  *val;       /* nnz */
+    int32_t memory;     /* ias_memory */
+    int32_t device;     /* HIP ordinal when memory == IAS_MEMORY_DEVICE */
+} ias_csr;
+
+/* CooMatrix (detail/format.h:17-29): row-sorted COO carrying row_offset. */
+typedef struct ias_coo {
+    int64_t rows, cols, nnz;
+    int64_t *row_offset; /* rows+1 */
+    int32_t *row;        /* nnz */
+    int32_t *col;        /* nnz */
+    double  *val;        /* nnz */
+    int32_t memory, device;
+    int32_t choice;      /* reference `choice`: 0 = infeasible under the size gate */
+    int32_t reserved;
+} ias_coo;
+
+/* EllMatrix (detail/format.h:66-76); col/val are rows x max_nnz_per_row,
+ * row-major, padding = column 0 / value 0.0 (malloc2d zero-fill). */
+typedef struct ias_ell {
+    int64_t rows, cols, nnz;
+    int32_t max_nnz_per_row;
+    int32_t choice;
+    int32_t *nnz_row;    /* rows */
+    int32_t *col;
+    double  *val;
+    int32_t memory, device;
+} ias_ell;
+
+/* DiaMatrix (detail/format.h:56-64); val is rows x num_diagonals row-major:
+ * val[i*nd + d] = A(i, i + diagonal_offsets[d]) (0.0 where out of range).
+ * diagonal_ind has rows+cols-1 entries: diagonal_ind[off + rows - 1] = slot
+ * of offset `off` (0 where the diagonal is absent, as the reference). */
+typedef struct ias_dia {
+    int64_t rows, cols;
+    int32_t num_diagonals;
+    int32_t choice;
+    int32_t *diagonal_offsets; /* num_diagonals, ascending */
+    int32_t *diagonal_ind;     /* rows + cols - 1 */
+    double  *val;
+    int32_t memory, device;
+} ias_dia;
+
+/* Per-call options. Zero-initialise and set what you need (ias_opts_default). */
+typedef struct ias_opts {
+    int32_t order;          /* ias_order */
+    int32_t output_memory;  /* ias_memory for C; -1 = same as A */
+    int32_t device;         /* HIP device used for compute; -1 = A's device, else 0 */
+    int32_t reserved0;
+    void   *stream;         /* hipStream_t; NULL = the plan's own stream */
+    struct ias_plan *plan;  /* optional workspace cache reused across calls */
+} ias_opts;
+
+/* Per-call measurements (device time by hipEvents on the compute stream). */
+typedef struct ias_report {
+    double  ms_total;       /* first kernel -> last byte of C written */
+    double  ms_analysis;    /* row products + binning */
+    double  ms_symbolic;    /* per-row nnz + scan */
+    double  ms_numeric;     /* accumulate + write C */
+    double  ms_upload;      /* host->device of A,B when given on the host */
+    double  ms_download;    /* device->host of C when returned on the host */
+    int64_t flops;          /* GetFlop (csr/common_csr.h:290-304): multiply pairs */
+    int64_t nnz_c;
+    int64_t max_row_products;
+    int64_t max_row_nnz;
+} ias_report;
+
+typedef struct ias_mtx_info {
+    int32_t is_pattern, is_real, is_integer, is_symmetric; /* main.cpp:171-189 */
+    int64_t rows, cols;
+    int64_t nnz_file;       /* entries listed in the file (nnzA_mtx_report) */
+} ias_mtx_info;
+
+typedef struct ias_plan ias_plan;
+
+/* ---------------------------------------------------------------- misc */
+int         ias_abi_version(void);
+const char *ias_status_string(ias_status s);
+/* Detail of the last failure on the calling thread ("" if none). */
+const char *ias_last_error(void);
+ias_status  ias_device_count(int32_t *count);
+void        ias_opts_default(ias_opts *opts);
+
+/* Workspace/stream holder; the analogue of the cuSPARSE handle the reference
+ * creates per call (GPU/detail/cusparse/common_cusparse.h:44-72). */
+ias_status ias_plan_create(ias_plan **plan, int32_t device, void *stream);
+ias_status ias_plan_destroy(ias_plan *plan);
+
+/* ---------------------------------------------------------------- memory */
+ias_status ias_csr_alloc(ias_csr *m, int64_t rows, int64_t cols, int64_t nnz,
+                         int32_t memory, int32_t device);
+ias_status ias_csr_copy(const ias_csr *src, ias_csr *dst, int32_t memory, int32_t device);
+ias_status ias_csr_free(ias_csr *m);   /* FreeCsrMatrix  csr/common_csr.h:307-317 */
+ias_status ias_coo_free(ias_coo *m);   /* FreeCooMatrix  coo/common_coo.h:185-195 */
+ias_status ias_ell_free(ias_ell *m);   /* FreeEllMatrix  ell/common_ell.h:232-244 */
+ias_status ias_dia_free(ias_dia *m);   /* FreeDiaMatrix  dia/common_dia.h:236-249 */
+ias_status ias_coo_copy(const ias_coo *src, ias_coo *dst, int32_t memory, int32_t device);
+ias_status ias_ell_copy(const ias_ell *src, ias_ell *dst, int32_t memory, int32_t device);
+ias_status ias_dia_copy(const ias_dia *src, ias_dia *dst, int32_t memory, int32_t device);
+
+/* ---------------------------------------------------------------- Matrix-Market I/O
+ * Reader semantics of main.cpp:143-458 + mmio.h:254-367: banner typecode,
+ * comment skipping, 1-based -> 0-based, pattern -> 1.0, integer -> double,
+ * symmetric/hermitian mirrored with the same value (skew NOT mirrored),
+ * stable counting sort by row in file order, duplicates kept, columns unsorted.
+ * Result is on the host. */
+ias_status ias_mtx_read(const char *path, ias_csr *A, ias_mtx_info *info);
+/* Two-file read exactly as main.cpp:139-458: B's row count is forced to A's
+ * column count (main.cpp:482) and B's own row count is ignored. */
+ias_status ias_mtx_read_pair(const char *path_a, const char *path_b, ias_csr *A, ias_csr *B,
+                             ias_mtx_info *info_a, ias_mtx_info *info_b);
+/* mm_write_mtx_crd (mmio.h:445-486): "%%MatrixMarket matrix coordinate real general". */
+ias_status ias_mtx_write(const char *path, const ias_csr *A);
+
+/* ---------------------------------------------------------------- format layer
+ * gate: the reference feasibility threshold (50 on CPU: coo/common_coo.h:37,
+ * dia/common_dia.h:56, ell/common_ell.h:47; 20 on GPU: GPU/detail/dia/
+ * common_dia.h:51 etc.); <= 0 disables the gate.  When the gate fails the
+ * output has choice = 0, no arrays, and IAS_ERROR_INFEASIBLE is returned.
+ * Inputs may be host or device; outputs land in the same memory. */
+ias_status ias_csr_to_coo(const ias_csr *A, ias_coo *out, double gate); /* CSRtoCOO coo:29-66 */
+ias_status ias_csr_to_ell(const ias_csr *A, ias_ell *out, double gate); /* CSRtoELL ell:30-77 */
+ias_status ias_csr_to_dia(const ias_csr *A, ias_dia *out, double gate); /* CSRtoDIA dia:29-96 */
+ias_status ias_coo_to_csr(const ias_coo *A, ias_csr *out);
+ias_status ias_ell_to_csr(const ias_ell *A, ias_csr *out);
+/* Every stored DIA position that is in range (explicit zeros included). */
+ias_status ias_dia_to_csr(const ias_dia *A, ias_csr *out);
+/* B = A^T, as mkl_dcsrcsc(job={0,0,0,0,0,1}) in GPU/main.cu:260-269; columns of
+ * each output row ascend (stable by source row). */
+ias_status ias_csr_transpose(const ias_csr *A, ias_csr *AT);
+
+/* size models of the report's memory_size column */
+double ias_sizeof_csr(const ias_csr *A); /* sizeofcsr csr/common_csr.h:196-202 */
+double ias_sizeof_coo(const ias_coo *A); /* sizeofcoo coo/common_coo.h:20-26 */
+double ias_sizeof_ell(const ias_ell *A); /* sizeofell ell/common_ell.h:21-27 */
+double ias_sizeof_dia(const ias_dia *A); /* sizeofdia dia/common_dia.h:20-26 */
+
+/* ---------------------------------------------------------------- SpGEMM hot path
+ * C = A * B.  C must be zero-initialised by the caller; the library allocates
+ * its arrays (memory per opts->output_memory) and the caller frees them.
+ * opts and report may be NULL. */
+ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_csr *C,
+                           const ias_opts *opts, ias_report *report);  /* CSR_MUL_CSR csr:85-193 */
+ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_coo *C,
+                           const ias_opts *opts, ias_report *report);  /* COO_MUL_COO coo:72-161 */
+ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_ell *C,
+                           const ias_opts *opts, ias_report *report);  /* ELL_MUL_ELL ell:80-189 */
+ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
+                           const ias_opts *opts, ias_report *report);  /* DIA_mul_DIA dia:101-195 */
+
+/* Two-phase form on device-resident CSR, the split the reference's GPU path
+ * uses (cusparseXcsrgemmNnz + cusparseDcsrgemm, GPU/detail/cusparse/
+ * common_cusparse.h:78-91).  nnz: analysis + symbolic + scan; the row pointer
+ * of C is written to row_ptr_c (device, rows+1) when non-NULL and kept in the
+ * plan otherwise.  compute: numeric phase into caller-provided device arrays
+ * C->row_ptr/col/val with capacity C->nnz (>= the nnz returned); it must
+ * follow an nnz call on the same plan with the same A and B. */
+ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, const ias_csr *B,
+                               int64_t *nnz_c, int64_t *row_ptr_c, ias_report *report);
+ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_csr *B,
+                                   ias_csr *C, int32_t order, ias_report *report);
+
+/* ---------------------------------------------------------------- verification */
+/* GetFlop (csr/common_csr.h:290-304): sum over stored A(i,j) of nnz(B row j). */
+ias_status ias_flops(const ias_csr *A, const ias_csr *B, int64_t *flops);
+/* verified_sum (main.cpp:753-755 etc.): sum of all stored values (sequential
+ * order on the host; DIA/ELL sum their padded arrays as the reference). */
+ias_status ias_sum_csr(const ias_csr *A, double *sum);
+ias_status ias_sum_coo(const ias_coo *A, double *sum);
+ias_status ias_sum_ell(const ias_ell *A, double *sum);
+ias_status ias_sum_dia(const ias_dia *A, double *sum);
+
+/* ---------------------------------------------------------------- multi-GPU helpers
+ * Row-block view [r0, r1) of A without copying (row_ptr is an offset view;
+ * kernels address col/val absolutely, so no rebasing is needed). */
+ias_status ias_csr_row_view(const ias_csr *A, int64_t r0, int64_t r1, ias_csr *view);
+/* Split A's rows into nparts contiguous blocks with near-equal products
+ * (flops prefix); bounds has nparts+1 entries. Host or device A. */
+ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int32_t nparts,
+                              int64_t *bounds);
+/* Add `offset` to every entry of a device row pointer (allgatherv fix-up). */
+ias_status ias_row_ptr_shift(int64_t *row_ptr, int64_t count, int64_t offset,
+                             int32_t device, void *stream);
+
+/* ---------------------------------------------------------------- synthetic inputs
+ * Deterministic host generators (counter-based splitmix64; identical on every
+ * machine).  value_mode 0: U(-1,1); 1: integers 1..9 (exact fp64 sums). */
+ias_status ias_gen_rmat(int32_t scale, double edge_factor, double a, double b, double c,
+                        uint64_t seed, int32_t value_mode, ias_csr *out);
+ias_status ias_gen_band(int64_t n, int32_t half_width, uint64_t seed, int32_t value_mode,
+                        ias_csr *out);
+ias_status ias_gen_ell(int64_t n, int32_t per_row, uint64_t seed, int32_t value_mode,
+                       ias_csr *out);
+
+/* ---------------------------------------------------------------- CPU baseline
+ * The reference's Algorithm 1, MKL_MUL_MKL (csr/common_csr.h:18-47):
+ * mkl_sparse_d_create_csr x2 + mkl_sparse_sp2m(FULL_MULT) + export, timed as
+ * main.cpp:746-748.  MKL is loaded at run time (dlopen libmkl_rt, GNU threading
+ * layer); IAS_ERROR_UNAVAILABLE if absent.  A, B on the host; C on the host
+ * (library-allocated); int32 (LP64) unless nnz needs ILP64, which is used then. */
+ias_status ias_mkl_available(int32_t *available, char *version, int32_t version_len);
+ias_status ias_mkl_sp2m(const ias_csr *A, const ias_csr *B, ias_csr *C, int32_t threads,
+                        double *ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IAS_H */

@@ -1,0 +1,301 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle restatement
+of the reference (oracle/ias_oracle.c) on the same seeded inputs.
+
+Bar: integer / index work bit-exact; values bit-exact too, because the HIP
+kernels sum every output entry in the reference's product order without FMA
+(the reference's CSR_MUL_CSR / COO_MUL_COO / ELL_MUL_ELL / DIA_mul_DIA
+semantics).  The MKL cross-check uses the north-star tolerance
+|dC| <= 1e-10 * max(|c|, sum|a_ik*b_kj|).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import ias
+import oracle_bind as ob
+
+pytestmark = pytest.mark.gpu
+
+SQUARE = ["dia.mtx", "small.mtx", "b1_ss.mtx", "Ragusa18.mtx", "LFAT5.mtx"]
+ALL = SQUARE + ["Trec5.mtx", "ch3-3-b2.mtx", "relat3.mtx", "sample.mtx"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if ias.device_count() < 1:
+        pytest.fail("no HIP device visible: the gpu tests must run on an MI355X box")
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.int64)
+
+
+def assert_csr_identical(got, ref, what=""):
+    assert got.rows == ref.rows and got.cols == ref.cols, what
+    np.testing.assert_array_equal(got.row_ptr, ref.row_ptr, err_msg=f"{what} row_ptr")
+    np.testing.assert_array_equal(got.col, ref.col, err_msg=f"{what} col order")
+    np.testing.assert_array_equal(bits(got.val), bits(ref.val), err_msg=f"{what} values (bitwise)")
+
+
+def sorted_form(m):
+    rp, col, val = m.row_ptr, m.col, m.val
+    oc, ov = np.empty_like(col), np.empty_like(val)
+    for i in range(m.rows):
+        s, e = rp[i], rp[i + 1]
+        o = np.argsort(col[s:e], kind="stable")
+        oc[s:e], ov[s:e] = col[s:e][o], val[s:e][o]
+    return oc, ov
+
+
+def transpose(m):
+    s = ias.HostCsr(m.rows, m.cols, m.row_ptr, m.col, m.val).struct()
+    t = ias.Csr()
+    ias.check(ias.lib.ias_csr_transpose(C.byref(s), C.byref(t)), "transpose")
+    return ias.csr_to_numpy(t)
+
+
+def cases_small():
+    """(name, A, B) synthetic cases at oracle-friendly sizes."""
+    out = []
+    out.append(("band4k", ias.gen_band(4096, 3, seed=7), None))
+    out.append(("band4k_int", ias.gen_band(4096, 3, seed=7, value_mode=1), None))
+    out.append(("ell8k", ias.gen_ell(8192, 16, seed=7), None))
+    out.append(("rmat12", ias.gen_rmat(12, 16, seed=1), None))
+    out.append(("rmat14_int", ias.gen_rmat(14, 20, seed=2, value_mode=1), None))
+    out.append(("rmat15", ias.gen_rmat(15, 8, seed=3), None))
+    # cancellation: A=[[1,1],[1,-1]] -> C has 4 stored entries, two of them 0.0
+    out.append(("cancel", ias.HostCsr(2, 2, np.array([0, 2, 4]), np.array([0, 1, 0, 1]),
+                                      np.array([1.0, 1.0, 1.0, -1.0])), None))
+    # duplicates inside rows, empty rows, unsorted columns
+    rp = np.array([0, 4, 4, 7, 9, 9])
+    col = np.array([3, 1, 3, 0, 2, 2, 4, 1, 0])
+    val = np.array([1.5, -2.0, 0.25, 3.0, 1.0, -1.0, 2.0, 0.5, -0.5])
+    out.append(("dups", ias.HostCsr(5, 5, rp, col, val), None))
+    # signed zeros: 0.0 * negative = -0.0 first product (CSR: 0.0 + -0.0 = +0.0)
+    out.append(("negzero", ias.HostCsr(2, 2, np.array([0, 2, 3]), np.array([0, 1, 1]),
+                                       np.array([0.0, 1.0, -3.0])), None))
+    return out
+
+
+def long_rows(n=40000, head=3000, per=10, seed=5):
+    """Row 0 has `head` entries into rows of `per` columns each: products beyond
+    every LDS bin, so the global-memory tables (symbolic and numeric) run."""
+    rng = np.random.default_rng(seed)
+    rows = [np.arange(head)] + [np.sort(rng.choice(n, per, replace=False)) for _ in range(n - 1)]
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.integers(1, 10, size=col.size).astype(np.float64)
+    return ias.HostCsr(n, n, rp, col, val)
+
+
+# ------------------------------------------------------------------ CSR
+@pytest.mark.parametrize("name", SQUARE)
+def test_csr_inputs_a_times_a(inputs_dir, name):
+    A, _ = ias.mtx_read(os.path.join(inputs_dir, name))
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, rep = ias.spgemm(A)
+    assert_csr_identical(got, ref, name)
+    assert rep.flops == ob.flops(ob.Mat.of(A), ob.Mat.of(A))
+    assert rep.nnz_c == ref.nnz
+
+
+@pytest.mark.parametrize("name", ALL)
+def test_csr_inputs_a_times_at(inputs_dir, name):
+    A, _ = ias.mtx_read(os.path.join(inputs_dir, name))
+    AT = transpose(A)
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(AT))
+    got, _ = ias.spgemm(A, AT)
+    assert_csr_identical(got, ref, name + " A*At")
+
+
+@pytest.mark.parametrize("case", cases_small(), ids=lambda c: c[0])
+def test_csr_synthetic(case):
+    name, A, B = case
+    B = A if B is None else B
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    got, rep = ias.spgemm(A, B)
+    assert_csr_identical(got, ref, name)
+    assert rep.flops == ob.flops(ob.Mat.of(A), ob.Mat.of(B))
+
+
+def test_csr_long_rows_global_tables():
+    A = long_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, rep = ias.spgemm(A)
+    assert rep.max_row_products > 21840 and rep.max_row_nnz > 5460
+    assert_csr_identical(got, ref, "long rows")
+
+
+@pytest.mark.parametrize("case", cases_small()[:6], ids=lambda c: c[0])
+def test_csr_sorted_order(case):
+    name, A, _ = case
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, _ = ias.spgemm(A, order=ias.ORDER_SORTED)
+    rc, rv = sorted_form(ref)
+    np.testing.assert_array_equal(got.row_ptr, ref.row_ptr)
+    np.testing.assert_array_equal(got.col, rc)
+    np.testing.assert_array_equal(bits(got.val), bits(rv))
+
+
+def test_csr_sorted_long_rows():
+    A = long_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, _ = ias.spgemm(A, order=ias.ORDER_SORTED)
+    rc, rv = sorted_form(ref)
+    np.testing.assert_array_equal(got.col, rc)
+    np.testing.assert_array_equal(bits(got.val), bits(rv))
+
+
+def test_csr_empty_and_zero_rows():
+    A = ias.HostCsr(3, 4, np.zeros(4, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    B = ias.HostCsr(4, 2, np.zeros(5, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    got, rep = ias.spgemm(A, B)
+    assert got.nnz == 0 and got.rows == 3 and got.cols == 2 and rep.flops == 0
+
+
+def test_csr_dimension_mismatch():
+    A = ias.gen_band(16, 1)
+    B = ias.HostCsr(8, 8, np.zeros(9, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    with pytest.raises(ias.IasError) as e:
+        ias.spgemm(A, B)
+    assert e.value.status == 2
+
+
+# ------------------------------------------------------------------ COO / ELL / DIA
+def _coo_of(A):
+    s = A.struct()
+    c = ias.Coo()
+    ias.check(ias.lib.ias_csr_to_coo(C.byref(s), C.byref(c), 0.0), "to_coo")
+    return c
+
+
+@pytest.mark.parametrize("case", cases_small(), ids=lambda c: c[0])
+def test_coo_synthetic(case):
+    name, A, _ = case
+    ref, ref_rows = ob.coo_mul_coo(ob.Mat.of(A), ob.Mat.of(A))
+    ca = _coo_of(A)
+    cc = ias.Coo()
+    o = ias.opts(output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_coo_mul_coo(C.byref(ca), C.byref(ca), C.byref(cc), C.byref(o), None), "coo")
+    n = cc.nnz
+    got_rp = ias._np(cc.row_offset, cc.rows + 1, np.int64)
+    got_r = ias._np(cc.row, n, np.int32)
+    got_c = ias._np(cc.col, n, np.int32)
+    got_v = ias._np(cc.val, n, np.float64)
+    ias.lib.ias_coo_free(C.byref(ca))
+    ias.lib.ias_coo_free(C.byref(cc))
+    np.testing.assert_array_equal(got_rp, ref.row_ptr)
+    np.testing.assert_array_equal(got_r, ref_rows)
+    np.testing.assert_array_equal(got_c, ref.col)
+    np.testing.assert_array_equal(bits(got_v), bits(ref.val))
+
+
+@pytest.mark.parametrize("case", cases_small(), ids=lambda c: c[0])
+def test_ell_synthetic(case):
+    name, A, _ = case
+    ref = ob.ell_mul_ell(ob.Mat.of(A), ob.Mat.of(A))
+    s = A.struct()
+    ea, ec = ias.Ell(), ias.Ell()
+    ias.check(ias.lib.ias_csr_to_ell(C.byref(s), C.byref(ea), 0.0), "to_ell")
+    o = ias.opts(output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_ell_mul_ell(C.byref(ea), C.byref(ea), C.byref(ec), C.byref(o), None), "ell")
+    K = ec.max_nnz_per_row
+    assert K == ref["K"] and ec.nnz == ref["nnz"]
+    got_n = ias._np(ec.nnz_row, ec.rows, np.int32)
+    got_c = ias._np(ec.col, ec.rows * K, np.int32).reshape(ec.rows, K)
+    got_v = ias._np(ec.val, ec.rows * K, np.float64).reshape(ec.rows, K)
+    ias.lib.ias_ell_free(C.byref(ea))
+    ias.lib.ias_ell_free(C.byref(ec))
+    np.testing.assert_array_equal(got_n, ref["nnz_row"])
+    np.testing.assert_array_equal(got_c, ref["col"])
+    np.testing.assert_array_equal(bits(got_v), bits(ref["val"]))
+
+
+DIA_CASES = [("band4k", lambda: ias.gen_band(4096, 3, seed=7)),
+             ("band_w1", lambda: ias.gen_band(1000, 1, seed=3, value_mode=1)),
+             ("dia.mtx", None), ("small.mtx", None), ("b1_ss.mtx", None)]
+
+
+@pytest.mark.parametrize("case", DIA_CASES, ids=lambda c: c[0])
+def test_dia(case, inputs_dir):
+    name, mk = case
+    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
+    ref = ob.dia_mul_dia(ob.Mat.of(A), ob.Mat.of(A))
+    s = A.struct()
+    da, dc = ias.Dia(), ias.Dia()
+    ias.check(ias.lib.ias_csr_to_dia(C.byref(s), C.byref(da), 0.0), "to_dia")
+    o = ias.opts(output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_dia_mul_dia(C.byref(da), C.byref(da), C.byref(dc), C.byref(o), None), "dia")
+    nd = dc.num_diagonals
+    assert nd == ref["nd"]
+    np.testing.assert_array_equal(ias._np(dc.diagonal_offsets, nd, np.int32), ref["offsets"])
+    np.testing.assert_array_equal(ias._np(dc.diagonal_ind, dc.rows + dc.cols - 1, np.int32), ref["ind"])
+    got_v = ias._np(dc.val, dc.rows * nd, np.float64).reshape(dc.rows, nd)
+    np.testing.assert_array_equal(bits(got_v), bits(ref["val"]))
+    ias.lib.ias_dia_free(C.byref(da))
+    ias.lib.ias_dia_free(C.byref(dc))
+
+
+# ------------------------------------------------------------------ device-resident two-phase
+def test_two_phase_device_resident():
+    A = ias.gen_rmat(14, 16, seed=4)
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    hs = A.struct()
+    dA = ias.Csr()
+    ias.check(ias.lib.ias_csr_copy(C.byref(hs), C.byref(dA), ias.MEMORY_DEVICE, 0), "copy")
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), 0, None), "plan")
+    try:
+        for _ in range(3):   # plan reuse across calls
+            nnz = C.c_int64(0)
+            ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(dA), C.byref(dA), C.byref(nnz), None, None), "nnz")
+            assert nnz.value == ref.nnz
+            dC = ias.Csr()
+            ias.check(ias.lib.ias_csr_alloc(C.byref(dC), A.rows, A.cols, nnz.value, ias.MEMORY_DEVICE, 0), "alloc")
+            ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(dA), C.byref(dA), C.byref(dC),
+                                                      ias.ORDER_REFERENCE, None), "compute")
+            got = ias.csr_to_numpy(dC)
+            assert_csr_identical(got, ref, "two-phase")
+    finally:
+        ias.lib.ias_plan_destroy(plan)
+        ias.lib.ias_csr_free(C.byref(dA))
+
+
+def test_row_views_concatenate():
+    """Row-block shards (the multi-GPU unit) concatenate to the 1-GPU result."""
+    A = ias.gen_rmat(13, 16, seed=9)
+    full, _ = ias.spgemm(A)
+    bounds = (C.c_int64 * 5)()
+    sa = A.struct()
+    ias.check(ias.lib.ias_partition_rows(C.byref(sa), C.byref(sa), 4, bounds), "partition")
+    cols, vals, lens = [], [], []
+    for k in range(4):
+        v = ias.Csr()
+        ias.check(ias.lib.ias_csr_row_view(C.byref(sa), bounds[k], bounds[k + 1], C.byref(v)), "view")
+        c, o = ias.Csr(), ias.opts(output_memory=ias.MEMORY_HOST, device=0)
+        ias.check(ias.lib.ias_csr_mul_csr(C.byref(v), C.byref(sa), C.byref(c), C.byref(o), None), "shard")
+        part = ias.csr_to_numpy(c)
+        cols.append(part.col); vals.append(part.val); lens.append(np.diff(part.row_ptr))
+    np.testing.assert_array_equal(np.concatenate(lens), np.diff(full.row_ptr))
+    np.testing.assert_array_equal(np.concatenate(cols), full.col)
+    np.testing.assert_array_equal(bits(np.concatenate(vals)), bits(full.val))
+
+
+# ------------------------------------------------------------------ MKL cross-check
+def test_against_mkl_tolerance():
+    ok, _ = ias.mkl_available()
+    if not ok:
+        pytest.skip("MKL runtime not present on this box")
+    A = ias.gen_rmat(14, 16, seed=2)
+    got, _ = ias.spgemm(A, order=ias.ORDER_SORTED)
+    mk, _ = ias.mkl_sp2m(A, A)
+    mc, mv = sorted_form(mk)
+    np.testing.assert_array_equal(got.row_ptr, mk.row_ptr)
+    np.testing.assert_array_equal(got.col, mc)
+    # |dC| <= 1e-10 * sum |a||b| (absolute products) per entry
+    absA = ias.HostCsr(A.rows, A.cols, A.row_ptr, A.col, np.abs(A.val))
+    bound, _ = ias.spgemm(absA, order=ias.ORDER_SORTED)
+    assert np.all(np.abs(got.val - mv) <= 1e-10 * np.maximum(np.abs(mv), bound.val) + 1e-300)
