@@ -77,6 +77,13 @@ struct Mkl {
             h = nullptr;
             return false;
         }
+        // Layers must be fixed before ANY other MKL call (even the version
+        // query), or MKL initialises with its Intel OpenMP layer, which next to
+        // libgomp returns a wrong C.
+        const char *e = getenv("IAS_MKL_ILP64");
+        iface = (e && atoi(e)) ? MKL_INTERFACE_ILP64 : MKL_INTERFACE_LP64;
+        if (set_interface_layer) set_interface_layer(iface);
+        set_threading_layer(MKL_THREADING_GNU);
         return true;
     }
 };
@@ -175,13 +182,6 @@ extern "C" ias_status ias_mkl_sp2m(const ias_csr *A, const ias_csr *B, ias_csr *
     if (!g_mkl.load()) {
         set_last_error("libmkl_rt not found (set IAS_MKL_PATH)");
         return IAS_ERROR_UNAVAILABLE;
-    }
-    if (g_mkl.iface < 0) {
-        // choose the index width once per process (MKL fixes it at first use)
-        const char *e = getenv("IAS_MKL_ILP64");
-        g_mkl.iface = (e && atoi(e)) ? MKL_INTERFACE_ILP64 : MKL_INTERFACE_LP64;
-        if (g_mkl.set_interface_layer) g_mkl.set_interface_layer(g_mkl.iface);
-        g_mkl.set_threading_layer(MKL_THREADING_GNU);
     }
     if (threads > 0 && g_mkl.set_num_threads) g_mkl.set_num_threads(threads);
     if (g_mkl.iface == MKL_INTERFACE_ILP64) return run<long long>(A, B, C, ms);

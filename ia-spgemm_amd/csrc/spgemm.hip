@@ -136,6 +136,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_rows(const int32_t *key, int6
 template <int TEAM, int LOG2S, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, const int32_t *list,
                                                              int32_t count, int32_t *nnz_row) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     __shared__ int32_t keys[TPW][1 << LOG2S];
     __shared__ Seg<TEAM, false> seg[TPW];
     __shared__ int scratch[TPW][16];
@@ -169,6 +170,7 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_global(Rows A, Rows B, const 
 template <int TEAM, int LOG2S, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_numeric_lds(Rows A, Rows B, const int32_t *list,
                                                             int32_t count, Out out) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     __shared__ int32_t keys[TPW][1 << LOG2S];
     __shared__ uint32_t meta[TPW][1 << LOG2S];
     __shared__ double vals[TPW][1 << LOG2S];
@@ -361,6 +363,7 @@ template <int TEAM, int CAP, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const int32_t *list, int32_t count,
                                                          const int64_t *ptr, const int32_t *len,
                                                          int64_t stride, int32_t *col, double *val) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     __shared__ int32_t sk[TPW][CAP];
     __shared__ double sv[TPW][CAP];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
@@ -533,7 +536,7 @@ ias_status Plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t co
     if ((c = hc.sym_count[2]) > 0)
         k_symbolic_lds<64, 8, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, nnz);
     if ((c = hc.sym_count[3]) > 0)
-        k_symbolic_lds<128, 10, 2><<<grid_for(c, 2), 256, 0, s>>>(A, B, lst(3), c, nnz);
+        k_symbolic_lds<128, 10, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, nnz);
     if ((c = hc.sym_count[4]) > 0)
         k_symbolic_lds<256, 12, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, nnz);
     if ((c = hc.sym_count[5]) > 0)
@@ -595,7 +598,7 @@ ias_status Plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_repor
     if ((c = num_count[2]) > 0)
         k_numeric_lds<64, 7, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, out);
     if ((c = num_count[3]) > 0)
-        k_numeric_lds<128, 9, 2><<<grid_for(c, 2), 256, 0, s>>>(A, B, lst(3), c, out);
+        k_numeric_lds<128, 9, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, out);
     if ((c = num_count[4]) > 0)
         k_numeric_lds<256, 11, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, out);
     if ((c = num_count[5]) > 0)
