@@ -590,6 +590,7 @@ extern "C" ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, cons
     if (row_ptr_c) {
         HIPC(hipMemcpyAsync(row_ptr_c, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
                             hipMemcpyDeviceToDevice, (hipStream_t)plan->stream));
+        HIPC(hipStreamSynchronize((hipStream_t)plan->stream));
     }
     return IAS_SUCCESS;
 }
@@ -618,6 +619,9 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
     IAS_TRY(plan->numeric(ra, rb, out, rep));
     if (order == IAS_ORDER_SORTED)
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, plan->max_nnz));
+    // C is complete when this returns (callers may read or free it at once,
+    // from any stream), as the reference's timer sync does (GPU/detail/utime.h).
+    HIPC(hipStreamSynchronize(s));
     return IAS_SUCCESS;
 }
 

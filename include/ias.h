@@ -225,7 +225,9 @@ ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
  * of C is written to row_ptr_c (device, rows+1) when non-NULL and kept in the
  * plan otherwise.  compute: numeric phase into caller-provided device arrays
  * C->row_ptr/col/val with capacity C->nnz (>= the nnz returned); it must
- * follow an nnz call on the same plan with the same A and B. */
+ * follow an nnz call on the same plan with the same A and B.  Both calls
+ * return only when their device work is complete (C may be read or freed
+ * from any stream right away). */
 ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, const ias_csr *B,
                                int64_t *nnz_c, int64_t *row_ptr_c, ias_report *report);
 ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_csr *B,
