@@ -195,20 +195,44 @@ extern "C" ias_status ias_csr_alloc(ias_csr *m, int64_t rows, int64_t cols, int6
     return IAS_SUCCESS;
 }
 
+// Copies rebase: a row view (row_ptr[0] != 0, col/val addressed absolutely,
+// see ias_csr_row_view) becomes a standalone matrix with row_ptr[0] == 0.
 extern "C" ias_status ias_csr_copy(const ias_csr *src, ias_csr *dst, int32_t memory,
                                    int32_t device) {
-    if (!src || !dst) return IAS_ERROR_INVALID_ARGUMENT;
+    if (!src || !dst || !src->row_ptr || src->rows < 0) return IAS_ERROR_INVALID_ARGUMENT;
+    int64_t ends[2] = {0, 0};
+    if (src->memory == IAS_MEMORY_DEVICE) {
+        IAS_TRY(dev_copy_d2h(&ends[0], src->row_ptr, sizeof(int64_t), src->device));
+        IAS_TRY(dev_copy_d2h(&ends[1], src->row_ptr + src->rows, sizeof(int64_t), src->device));
+    } else {
+        ends[0] = src->row_ptr[0];
+        ends[1] = src->row_ptr[src->rows];
+    }
+    const int64_t base = ends[0], nnz = ends[1] - ends[0];
+    if (nnz < 0) return IAS_ERROR_INVALID_ARGUMENT;
     ias_csr t{};
-    t.rows = src->rows; t.cols = src->cols; t.nnz = src->nnz; t.memory = memory; t.device = device;
+    t.rows = src->rows; t.cols = src->cols; t.nnz = nnz; t.memory = memory; t.device = device;
     void *a = nullptr, *b = nullptr, *c = nullptr;
     ias_status s;
     if ((s = move_bytes(&a, src->row_ptr, sizeof(int64_t) * (src->rows + 1), src->memory, src->device, memory, device)) ||
-        (s = move_bytes(&b, src->col, sizeof(int32_t) * src->nnz, src->memory, src->device, memory, device)) ||
-        (s = move_bytes(&c, src->val, sizeof(double) * src->nnz, src->memory, src->device, memory, device))) {
+        (s = move_bytes(&b, src->col ? src->col + base : nullptr, sizeof(int32_t) * nnz, src->memory, src->device, memory, device)) ||
+        (s = move_bytes(&c, src->val ? src->val + base : nullptr, sizeof(double) * nnz, src->memory, src->device, memory, device))) {
         release(a, memory, device); release(b, memory, device); release(c, memory, device);
         return s;
     }
     t.row_ptr = (int64_t *)a; t.col = (int32_t *)b; t.val = (double *)c;
+    if (base != 0) {
+        if (memory == IAS_MEMORY_DEVICE) {
+            s = ias_shift_device(t.row_ptr, src->rows + 1, -base, nullptr);
+            if (s == IAS_SUCCESS && hipDeviceSynchronize() != hipSuccess) s = IAS_ERROR_DEVICE;
+        } else {
+            for (int64_t i = 0; i <= src->rows; ++i) t.row_ptr[i] -= base;
+        }
+        if (s != IAS_SUCCESS) {
+            release(a, memory, device); release(b, memory, device); release(c, memory, device);
+            return s;
+        }
+    }
     *dst = t;
     return IAS_SUCCESS;
 }
@@ -342,6 +366,28 @@ struct Staged {
     }
 };
 
+// A CSR operand on the compute device: the caller's when already there, else
+// a rebased copy owned (and freed) by this holder.
+struct StagedCsr {
+    ias_csr own{};
+    const ias_csr *use = nullptr;
+    bool owned = false;
+    ~StagedCsr() {
+        if (owned) ias_csr_free(&own);
+    }
+    ias_status stage(const ias_csr *m, int device) {
+        if (m->memory == IAS_MEMORY_DEVICE && m->device == device) {
+            use = m;
+            return IAS_SUCCESS;
+        }
+        IAS_TRY(ias_csr_copy(m, &own, IAS_MEMORY_DEVICE, device));
+        owned = true;
+        use = &own;
+        return IAS_SUCCESS;
+    }
+    const ias_csr *get() const { return use; }
+};
+
 ias_opts resolve(const ias_opts *opts) {
     ias_opts o;
     ias_opts_default(&o);
@@ -380,23 +426,17 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     HIPC(hipSetDevice(plan->device));
     hipStream_t s = (hipStream_t)plan->stream;
 
-    Staged st;
-    const int64_t *ap, *bp;
-    const int32_t *ac, *bc;
-    const double *av, *bv;
-    HIPC(hipEventRecord(plan->ev[5], s));
-    IAS_TRY(st.stage(A->row_ptr, A->rows + 1, A->memory, A->device, plan->device, &ap));
-    IAS_TRY(st.stage(A->col, A->nnz, A->memory, A->device, plan->device, &ac));
-    IAS_TRY(st.stage(A->val, A->nnz, A->memory, A->device, plan->device, &av));
-    if (B == A) {
-        bp = ap; bc = ac; bv = av;
-    } else {
-        IAS_TRY(st.stage(B->row_ptr, B->rows + 1, B->memory, B->device, plan->device, &bp));
-        IAS_TRY(st.stage(B->col, B->nnz, B->memory, B->device, plan->device, &bc));
-        IAS_TRY(st.stage(B->val, B->nnz, B->memory, B->device, plan->device, &bv));
+    // Operands not resident on the compute device are copied there (rebased,
+    // so host row views work); resident ones, views included, are used as-is.
+    StagedCsr sa, sb;
+    IAS_TRY(sa.stage(A, plan->device));
+    const ias_csr *dA = sa.get(), *dB = dA;
+    if (B != A) {
+        IAS_TRY(sb.stage(B, plan->device));
+        dB = sb.get();
     }
-    dev::Rows ra{ap, nullptr, 0, ac, av};
-    dev::Rows rb{bp, nullptr, 0, bc, bv};
+    dev::Rows ra{dA->row_ptr, nullptr, 0, dA->col, dA->val};
+    dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
     IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
     const int64_t nnz = plan->nnz_total;
 
