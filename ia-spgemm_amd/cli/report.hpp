@@ -1,0 +1,97 @@
+// report.hpp — shared pieces of the drop-in CLIs: timers, the reference's
+// print_csr layout (csr/common_csr.h:213-233) and its per-algorithm report
+// block (main.cpp:968-1000), plus the format selector.
+#pragma once
+
+#include "ias.h"
+
+#include <sys/time.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+namespace cli {
+
+inline double now_ms() {
+    timeval t;
+    gettimeofday(&t, nullptr);
+    return t.tv_sec * 1000.0 + t.tv_usec / 1000.0;
+}
+
+inline void die(const char *what, ias_status s) {
+    fprintf(stderr, "%s: %s (%s)\n", what, ias_status_string(s), ias_last_error());
+    exit(1);
+}
+
+#define CLI_TRY(what, expr)                 \
+    do {                                    \
+        ias_status _s = (expr);             \
+        if (_s != IAS_SUCCESS) cli::die(what, _s); \
+    } while (0)
+
+// print_csr: "row:%d col:%d nnz:%d", then row pointers, columns, "%.2lf," values.
+inline void print_csr(const ias_csr &m) {
+    ias_csr h{};
+    const ias_csr *p = &m;
+    if (m.memory == IAS_MEMORY_DEVICE) {
+        CLI_TRY("copy", ias_csr_copy(&m, &h, IAS_MEMORY_HOST, 0));
+        p = &h;
+    }
+    printf("row:%lld col:%lld nnz:%lld\n", (long long)p->rows, (long long)p->cols, (long long)p->nnz);
+    for (int64_t i = 0; i <= p->rows; ++i) printf("%lld,", (long long)p->row_ptr[i]);
+    printf("\n");
+    for (int64_t i = 0; i < p->nnz; ++i) printf("%d,", p->col[i]);
+    printf("\n");
+    for (int64_t i = 0; i < p->nnz; ++i) printf("%.2lf,", p->val[i]);
+    printf("\n");
+    if (p == &h) ias_csr_free(&h);
+}
+
+struct AlgResult {
+    double run_ms = 0, trans_ms = 0, mem = 0, sum = 0;
+};
+
+// main.cpp:968-1000 (trans_time printed from defined values; the reference
+// indexes a 3-element array out of bounds there).
+inline int report(const std::vector<AlgResult> &r, long long flops, bool speedup, bool trans) {
+    std::vector<double> sp(r.size(), 0.0);
+    double best = 0.0;
+    int best_i = -1;
+    for (size_t i = 0; i < r.size(); ++i) {
+        sp[i] = r[i].run_ms == 0.0 ? 0.0 : r[0].run_ms / r[i].run_ms;
+        if (best < sp[i]) {
+            best = sp[i];
+            best_i = (int)i;
+        }
+    }
+    for (size_t i = 0; i < r.size(); ++i) {
+        printf("------------------------------\n");
+        printf("Algorithm %d:\n", (int)i + 1);
+        printf("run_time: %lf\n", r[i].run_ms);
+        if (trans) printf("trans_time: %lf\n", r[i].trans_ms);
+        printf("memory_size: %lf\n", r[i].mem);
+        printf("verified_sum: %lf\n", r[i].sum);
+        printf("Gflops: %lf\n", r[i].run_ms == 0.0 ? 0.0 : (flops * 2.0) / (r[i].run_ms * 1000000));
+        if (speedup) printf("Speedup: %lf\n", sp[i]);
+    }
+    printf("------------------------------\n");
+    return best_i;
+}
+
+// Format selector (the "input-aware" choice).  MatNet needs
+// Keras, which is not available; this deterministic rule uses the same
+// feature families (GetInfo1 row statistics, GetInfo2 DIA fill, GetInfo3 ELL
+// fill): banded -> DIA, uniform rows -> ELL, else the CSR hash path.
+// Returns a 0-based algorithm index into {MKL, CSR, DIA, ELL, COO}.
+inline int select_format(const ias_csr &A, bool dia_ok, double dia_fill, bool ell_ok, double ell_fill) {
+    (void)A;
+    if (dia_ok && dia_fill >= 0.5) return 2;
+    if (ell_ok && ell_fill >= 0.9) return 3;
+    return 1;
+}
+
+}  // namespace cli

@@ -1,0 +1,82 @@
+// spgemm-gpu — drop-in for IA-SPGEMM-GPU_release/main.cu (the `spgemm-gpu`
+// program).  Reads one .mtx and reports the GPU algorithms; the reference's
+// Algorithm 1 (CUSP ESC, main.cu:467-505) and Algorithm 2 (cuSPARSE csrgemm,
+// main.cu:508-523) are replaced by this engine's two output orders:
+//   1 IAS row-wise hash, reference order (byte-identical to CSR_MUL_CSR)
+//   2 IAS row-wise hash + per-row sort (sorted columns, as csrgemm emits)
+// Usage: spgemm-gpu A.mtx [--aat] [--rand10] [--seed N] [--mtx-out C.mtx]
+//   default C = A*A (the README's contract); --aat builds B = A^T as
+//   main.cu:260-269 (mkl_dcsrcsc); --rand10 replaces values by rand()%10 as
+//   main.cu:236-243, seeded by --seed (the reference seeds with time(NULL)).
+#include "ias.h"
+#include "report.hpp"
+
+#include <cstring>
+
+using cli::AlgResult;
+
+int main(int argc, char **argv) {
+    const char *file = nullptr, *out_path = nullptr;
+    bool aat = false, rand10 = false;
+    unsigned seed = 0;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--aat")) aat = true;
+        else if (!strcmp(argv[i], "--rand10")) rand10 = true;
+        else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = (unsigned)atoi(argv[++i]);
+        else if (!strcmp(argv[i], "--mtx-out") && i + 1 < argc) out_path = argv[++i];
+        else if (!file) file = argv[i];
+    }
+    if (!file) {
+        std::printf("please use command like this : ./spgemm-gpu ./sample.mtx\n");
+        return 0;
+    }
+    ias_csr A{}, B{};
+    ias_mtx_info info{};
+    CLI_TRY("read", ias_mtx_read(file, &A, &info));
+    if (rand10) {
+        srand(seed);
+        for (int64_t i = 0; i < A.nnz; ++i) A.val[i] = rand() % 10;
+    }
+    if (aat) CLI_TRY("transpose", ias_csr_transpose(&A, &B));
+    else CLI_TRY("copy", ias_csr_copy(&A, &B, IAS_MEMORY_HOST, 0));
+    int64_t flops = 0;
+    CLI_TRY("flops", ias_flops(&A, &B, &flops));
+
+    const bool ell_ok = true;
+    ias_ell Ae{};
+    double ell_fill = 0;
+    if (ias_csr_to_ell(&A, &Ae, 20.0) == IAS_SUCCESS)
+        ell_fill = Ae.max_nnz_per_row ? (double)A.nnz / ((double)Ae.max_nnz_per_row * A.rows) : 0;
+    ias_ell_free(&Ae);
+    const int chosen = cli::select_format(A, false, 0.0, ell_ok, ell_fill) == 1 ? 0 : 1;
+    std::printf("The Chosen One = Algorithm %d\n", chosen + 1);
+
+    ias_csr dA{}, dB{};
+    CLI_TRY("upload", ias_csr_copy(&A, &dA, IAS_MEMORY_DEVICE, 0));
+    CLI_TRY("upload", ias_csr_copy(&B, &dB, IAS_MEMORY_DEVICE, 0));
+    ias_opts o;
+    ias_opts_default(&o);
+    o.output_memory = IAS_MEMORY_DEVICE;
+    o.device = 0;
+    CLI_TRY("plan", ias_plan_create(&o.plan, 0, nullptr));
+    std::vector<AlgResult> r(2);
+    for (int alg = 0; alg < 2; ++alg) {
+        o.order = alg == 0 ? IAS_ORDER_REFERENCE : IAS_ORDER_SORTED;
+        ias_csr C{};
+        CLI_TRY("spgemm", ias_csr_mul_csr(&dA, &dB, &C, &o, nullptr));   // warm-up
+        ias_csr_free(&C);
+        ias_report rep{};
+        CLI_TRY("spgemm", ias_csr_mul_csr(&dA, &dB, &C, &o, &rep));
+        r[alg].run_ms = rep.ms_total;   // device time (hipEvent), as the reference's cudaEvent timer
+        r[alg].mem = ias_sizeof_csr(&C);
+        ias_sum_csr(&C, &r[alg].sum);
+        if (alg == 0 && out_path) CLI_TRY("write", ias_mtx_write(out_path, &C));
+        ias_csr_free(&C);
+    }
+    ias_plan_destroy(o.plan);
+    cli::report(r, (long long)flops, false, false);
+    std::printf("MatNet predicts Algorithm %s is optimal\n", chosen == 0 ? "IAS-hash" : "IAS-sorted");
+    ias_csr_free(&dA); ias_csr_free(&dB);
+    ias_csr_free(&A); ias_csr_free(&B);
+    return 0;
+}
