@@ -1,7 +1,7 @@
 // spgemm.hip — kernels and host engine of the row-wise SpGEMM hot path
 // (replaces CSR_MUL_CSR / COO_MUL_COO / ELL_MUL_ELL of the reference and the
 // CUSP / cuSPARSE calls of GPU/main.cu:467-523).  See spgemm_kernels.hpp for
-// the per-row algorithm and DESIGN.md for the pipeline and its roofline.
+// the per-row algorithm and DESIGN.md §4 for the pipeline and its roofline.
 #include "spgemm_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
@@ -23,18 +23,16 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
                                                            unsigned long long *flops,
                                                            int32_t *max_prod) {
     __shared__ int64_t start[AN_BLOCK];
-    __shared__ int64_t pref[AN_BLOCK + 1];
+    __shared__ int32_t pref[AN_BLOCK + 1];
     __shared__ unsigned long long acc[AN_BLOCK];
     __shared__ int scratch[8];
     const int t = threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.x * AN_BLOCK;
-    const int64_t r = r0 + t;
+    const int64_t r = (int64_t)blockIdx.x * AN_BLOCK + t;
     int64_t s = 0;
     int32_t n = 0;
     if (r < rows) A.row(r, s, n);
     start[t] = s;
     acc[t] = 0;
-    // block exclusive scan of n (int64 to be safe)
     {
         int tot;
         const int ex = Team<AN_BLOCK>::excl_sum(n, tot, scratch);
@@ -42,15 +40,9 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
         if (t == 0) pref[AN_BLOCK] = tot;
     }
     __syncthreads();
-    const int64_t E = pref[AN_BLOCK];
-    for (int64_t e = t; e < E; e += AN_BLOCK) {
-        // row of entry e: last k with pref[k] <= e
-        int lo = 0, hi = AN_BLOCK;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (pref[mid] <= e) lo = mid;
-            else hi = mid;
-        }
+    const int32_t E = pref[AN_BLOCK];
+    for (int32_t e = t; e < E; e += AN_BLOCK) {
+        const int lo = seg_find(pref, AN_BLOCK, e);
         const int32_t j = A.col[start[lo] + (e - pref[lo])];
         int64_t bs;
         int32_t bn;
@@ -58,13 +50,13 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
         atomicAdd(&acc[lo], (unsigned long long)bn);
     }
     __syncthreads();
-    unsigned long long mine = acc[t];
-    if (r < rows) prod[r] = (int32_t)min(mine, (unsigned long long)INT32_MAX);
-    // block reductions
+    const unsigned long long mine = acc[t];
+    const int mx0 = (int)min(mine, (unsigned long long)INT32_MAX);
+    if (r < rows) prod[r] = mx0;
     __shared__ unsigned long long red_sum[AN_BLOCK / WAVE];
     __shared__ int red_max[AN_BLOCK / WAVE];
     unsigned long long sm = (r < rows) ? mine : 0ull;
-    int mx = (r < rows) ? (int)min(mine, (unsigned long long)INT32_MAX) : 0;
+    int mx = (r < rows) ? mx0 : 0;
     for (int d = WAVE / 2; d > 0; d >>= 1) {
         sm += __shfl_down(sm, d);
         mx = max(mx, __shfl_down(mx, d));
@@ -89,107 +81,170 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
 // ---------------------------------------------------------------- binning
 constexpr int BIN_BLOCK = 256;
 
-// key[i] -> bin; bin 0 = key 0 (no list, zero_out[i] = 0 when given);
-// bins 1..nbins-2 = LDS bins by upper bound; bin nbins-1 = global table,
-// whose rows also get a workspace offset of nextpow2(ceil(key*3/2)) slots.
+__device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
+    return (uint32_t)((key + cap - 1) / cap);
+}
+
+// key[i] -> bin (BinSpec).  LDS and wide bins get row lists; the partition
+// bin gets its rows listed AND one (row << 32 | part) work item per
+// partition; FT rows get a first-touch bitmap offset; wide rows a
+// global-table offset of nextpow2(ceil(key*3/2)) slots.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_rows(const int32_t *key, int64_t rows,
                                                         BinSpec spec, int32_t *lists,
-                                                        int32_t *counts,
-                                                        unsigned long long *ws_slots,
-                                                        int64_t *ws_off, int32_t *zero_out) {
+                                                        unsigned long long *items,
+                                                        int64_t *bm_off, int64_t *ws_off,
+                                                        int32_t *nnz_row, Counters *cnt) {
     __shared__ int hist[MAX_BINS];
     __shared__ int base[MAX_BINS];
     const int t = threadIdx.x;
     if (t < MAX_BINS) hist[t] = 0;
     __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + t;
+    const int part_bin = spec.nlds + 1, wide_bin = spec.nlds + 2;
     int b = -1, local = 0;
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
         if (k <= 0) {
             b = 0;
-            if (zero_out) zero_out[r] = 0;
+            if (spec.zero_nnz) nnz_row[r] = 0;
         } else {
-            b = spec.nbins - 1;
-            for (int i = 1; i < spec.nbins - 1; ++i)
-                if (k <= spec.upper[i]) { b = i; break; }
+            if (spec.wide_min > 0 && k >= spec.wide_min) {
+                b = wide_bin;
+            } else {
+                b = part_bin;
+                for (int i = 1; i <= spec.nlds; ++i)
+                    if (k <= spec.upper[i]) {
+                        b = i;
+                        break;
+                    }
+            }
             local = atomicAdd(&hist[b], 1);
         }
     }
     __syncthreads();
-    if (t < spec.nbins && t > 0 && hist[t] > 0) base[t] = atomicAdd(&counts[t], hist[t]);
+    if (t > 0 && t < MAX_BINS && hist[t] > 0) base[t] = atomicAdd(&cnt->count[t], hist[t]);
     __syncthreads();
     if (b > 0) {
         const int pos = base[b] + local;
         lists[(int64_t)b * rows + pos] = (int32_t)r;
-        if (b == spec.nbins - 1) {
+        if (b == part_bin) {
+            const uint32_t np = nparts_of(k, spec.part_cap);
+            const unsigned long long at = atomicAdd(&cnt->items, (unsigned long long)np);
+            for (uint32_t q = 0; q < np; ++q) items[at + q] = ((unsigned long long)r << 32) | q;
+            if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
+            if (spec.zero_nnz) nnz_row[r] = 0;
+        } else if (b == wide_bin) {
             const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
             unsigned long long S = 1;
             while (S < need) S <<= 1;
-            ws_off[pos] = (int64_t)atomicAdd(ws_slots, S);
+            ws_off[pos] = (int64_t)atomicAdd(&cnt->ws_slots, S);
         }
     }
 }
 
-// ---------------------------------------------------------------- per-bin kernels
-template <int TEAM, int LOG2S, int TPW>
+// ---------------------------------------------------------------- symbolic kernels
+template <int TEAM, int K, int LOG2S, int SEG, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, const int32_t *list,
                                                              int32_t count, int32_t *nnz_row) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     __shared__ int32_t keys[TPW][1 << LOG2S];
-    __shared__ Seg<TEAM, false> seg[TPW];
-    __shared__ int scratch[TPW][16];
+    __shared__ Seg<SEG, false> seg[TPW];
+    __shared__ int scratch[TPW][64];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
     const int64_t row = idx < count ? list[idx] : -1;
-    KeyTable tb{keys[team], (uint32_t)LOG2S};
-    const int32_t n = symbolic_row<TEAM>(A, B, row, tb, seg[team], scratch[team]);
+    SymTable<false> tb{keys[team], nullptr, (uint32_t)LOG2S};
+    const int32_t n = symbolic_row<TEAM, K, SEG, false>(A, B, row, tb, 0, 1, seg[team], scratch[team],
+                                                        nullptr, nullptr);
     if (row >= 0 && Team<TEAM>::lane() == 0) nnz_row[row] = n;
 }
 
-template <int TEAM>
-__global__ __launch_bounds__(TEAM) void k_symbolic_global(Rows A, Rows B, const int32_t *list,
-                                                          const int64_t *ws_off,
-                                                          const int32_t *prod, int32_t count,
-                                                          int32_t *ws, int32_t *nnz_row) {
-    __shared__ Seg<TEAM, false> seg;
-    __shared__ int scratch[16];
-    const int64_t idx = blockIdx.x;
-    if (idx >= count) return;
-    const int64_t row = list[idx];
-    const unsigned long long need =
-        (unsigned long long)prod[row] + ((unsigned long long)prod[row] + 1) / 2;
-    uint32_t l2 = 0;
-    while ((1ull << l2) < need) ++l2;
-    KeyTable tb{ws + ws_off[idx], l2};
-    const int32_t n = symbolic_row<TEAM>(A, B, row, tb, seg, scratch);
-    if (threadIdx.x == 0) nnz_row[row] = n;
+// One workgroup per (row, hash partition): distinct columns of the partition
+// (added to nnz_row) and the first-touch bits of the row's bitmap.
+template <int TEAM, int K, int LOG2S, int SEG>
+__global__ __launch_bounds__(TEAM) void k_symbolic_part(Rows A, Rows B, const unsigned long long *items,
+                                                        const int32_t *prod, int32_t part_cap,
+                                                        Bitmap bm, int32_t *nnz_row, int *overflow) {
+    __shared__ int32_t keys[1 << LOG2S];
+    __shared__ uint32_t minp[1 << LOG2S];
+    __shared__ Seg<SEG, false> seg;
+    __shared__ int scratch[64];
+    const unsigned long long it = items[blockIdx.x];
+    const int64_t row = (int64_t)(it >> 32);
+    const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
+    const uint32_t np = nparts_of(prod[row], part_cap);
+    SymTable<true> tb{keys, minp, (uint32_t)LOG2S};
+    const int32_t n = symbolic_row<TEAM, K, SEG, true>(A, B, row, tb, part, np, seg, scratch,
+                                                       bm.bits + bm.off[row], overflow);
+    if (threadIdx.x == 0 && n > 0) atomicAdd(&nnz_row[row], n);
 }
 
-template <int TEAM, int LOG2S, int TPW>
+// Exclusive popcount prefix of each partitioned row's first-touch bitmap.
+__global__ __launch_bounds__(256) void k_bitmap_prefix(const int32_t *list, int32_t count,
+                                                       const int32_t *prod, Bitmap bm) {
+    __shared__ int scratch[8];
+    const int64_t row = list[blockIdx.x];
+    const int64_t W = (prod[row] + 31) / 32;
+    const uint32_t *bits = bm.bits + bm.off[row];
+    uint32_t *pref = bm.pref + bm.off[row];
+    int carry = 0;
+    for (int64_t w0 = 0; w0 < W; w0 += 256) {
+        const int64_t w = w0 + threadIdx.x;
+        const int c = w < W ? __popc(bits[w]) : 0;
+        int tot;
+        const int ex = Team<256>::excl_sum(c, tot, scratch);
+        if (w < W) pref[w] = (uint32_t)(carry + ex);
+        carry += tot;
+    }
+}
+
+// ---------------------------------------------------------------- numeric kernels
+template <int TEAM, int K, int LOG2S, int SEG, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_numeric_lds(Rows A, Rows B, const int32_t *list,
                                                             int32_t count, Out out) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    constexpr int PER = (1 << LOG2S) / TEAM;
+    static_assert(PER >= 1 && PER <= 8, "emission keeps S/TEAM slots per lane in registers");
     __shared__ int32_t keys[TPW][1 << LOG2S];
     __shared__ uint32_t meta[TPW][1 << LOG2S];
     __shared__ double vals[TPW][1 << LOG2S];
-    __shared__ Seg<TEAM, true> seg[TPW];
-    __shared__ int scratch[TPW][16];
+    __shared__ Seg<SEG, true> seg[TPW];
+    __shared__ int scratch[TPW][64];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
     const int64_t row = idx < count ? list[idx] : -1;
     NumTable<false> tb{keys[team], meta[team], vals[team], (uint32_t)LOG2S};
-    numeric_row<TEAM, false>(A, B, row, tb, seg[team], scratch[team], out);
+    numeric_row<TEAM, K, SEG, false, false, PER>(A, B, row, tb, 0, 1, nullptr, nullptr, seg[team],
+                                                  scratch[team], out, 0, nullptr);
 }
 
-template <int TEAM>
+template <int TEAM, int K, int LOG2S, int SEG>
+__global__ __launch_bounds__(TEAM) void k_numeric_part(Rows A, Rows B, const unsigned long long *items,
+                                                       const int32_t *nnz_row, int32_t part_cap,
+                                                       Bitmap bm, Out out, int *overflow) {
+    __shared__ int32_t keys[1 << LOG2S];
+    __shared__ uint32_t meta[1 << LOG2S];
+    __shared__ double vals[1 << LOG2S];
+    __shared__ Seg<SEG, true> seg;
+    __shared__ int scratch[64];
+    const unsigned long long it = items[blockIdx.x];
+    const int64_t row = (int64_t)(it >> 32);
+    const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
+    const int32_t nnz = nnz_row[row];
+    const uint32_t np = nparts_of(nnz, part_cap);
+    NumTable<false> tb{keys, meta, vals, (uint32_t)LOG2S};
+    numeric_row<TEAM, K, SEG, false, true, 1>(A, B, row, tb, part, np, bm.bits + bm.off[row],
+                                              bm.pref + bm.off[row], seg, scratch, out, nnz, overflow);
+}
+
+template <int TEAM, int K, int SEG>
 __global__ __launch_bounds__(TEAM) void k_numeric_global(Rows A, Rows B, const int32_t *list,
                                                          const int64_t *ws_off,
                                                          const int32_t *nnz_row, int32_t count,
                                                          char *ws, Out out) {
-    __shared__ Seg<TEAM, true> seg;
-    __shared__ int scratch[16];
+    __shared__ Seg<SEG, true> seg;
+    __shared__ int scratch[64];
     const int64_t idx = blockIdx.x;
     if (idx >= count) return;
     const int64_t row = list[idx];
@@ -197,13 +252,13 @@ __global__ __launch_bounds__(TEAM) void k_numeric_global(Rows A, Rows B, const i
     const unsigned long long need = k + (k + 1) / 2;
     uint32_t l2 = 0;
     while ((1ull << l2) < need) ++l2;
-    // slot layout inside the row's region of 16-byte words: [keys | meta | vals]
-    // region = S * 16 bytes: keys S*4, pad to 8, meta S*8 ... kept simple:
+    // region of S * 20 bytes: keys (4 S) | meta (8 S) | vals (8 S)
     const uint64_t S = 1ull << l2;
     char *base = ws + (uint64_t)ws_off[idx] * 20ull;
     NumTable<true> tb{(int32_t *)base, (unsigned long long *)(base + S * 4ull),
                       (double *)(base + S * 12ull), l2};
-    numeric_row<TEAM, true>(A, B, row, tb, seg, scratch, out);
+    numeric_row<TEAM, K, SEG, true, false, 1>(A, B, row, tb, 0, 1, nullptr, nullptr, seg, scratch,
+                                              out, 0, nullptr);
 }
 
 // ---------------------------------------------------------------- scan
@@ -319,7 +374,6 @@ __global__ void k_fill_rows(const int64_t *ptr, int64_t rows, int32_t *row_idx) 
         row_idx[e] = (int32_t)r;
 }
 
-
 // ---------------------------------------------------------------- row sort
 // IAS_ORDER_SORTED: bitonic sort of (col, val) per row, in LDS up to 8192
 // entries, in a per-row global workspace beyond.  Columns of a row are
@@ -422,17 +476,38 @@ __global__ void k_row_len(const int64_t *ptr, int64_t rows, int32_t *len) {
 // =================================================================== host engine
 using namespace ias;
 using namespace ias::dev;
-using Plan = ias_plan;
 
-// Bin tables.  Symbolic bins by products, numeric bins by nnz; the table of a
-// bin holds up to `upper` keys at load <= 2/3 (S >= 1.5 * upper).
-static const int SYM_UPPER[] = {0, 40, 170, 680, 2730, 10920, 21840};   // + global
-static const int NUM_UPPER[] = {0, 20, 85, 340, 1365, 2730, 5460};     // + global
+// Bin tables.  Symbolic bins by products, keys-only LDS tables
+// at load <= 2/3; rows beyond 5460 products are hash-partitioned (4096
+// products per partition, 8192-slot key+first-touch tables) and get a
+// first-touch bitmap.  Numeric bins by nnz with 16-byte slots; rows beyond
+// 5460 nnz are hash-partitioned (4096 per partition); rows at >= 2^19 - 1 nnz
+// (beyond the 19-bit rank field) use a per-row table in global memory.
+constexpr int32_t LDS_MAX = 5460;
+constexpr int32_t PART_CAP = 4096;
+constexpr int32_t WIDE_MIN = (1 << 19) - 1;
 
-static BinSpec make_spec(const int *upper, int n_lds) {
+static BinSpec sym_spec() {
     BinSpec s{};
-    s.nbins = n_lds + 2;
-    for (int i = 0; i <= n_lds; ++i) s.upper[i] = upper[i];
+    s.nlds = 5;
+    const int32_t u[] = {0, 64, 256, 1024, 2730, LDS_MAX};
+    for (int i = 0; i <= 5; ++i) s.upper[i] = u[i];
+    s.part_cap = PART_CAP;
+    s.wide_min = 0;
+    s.ft = 1;
+    s.zero_nnz = 1;
+    return s;
+}
+
+static BinSpec num_spec() {
+    BinSpec s{};
+    s.nlds = 6;
+    const int32_t u[] = {0, 16, 64, 256, 1024, 2730, LDS_MAX};
+    for (int i = 0; i <= 6; ++i) s.upper[i] = u[i];
+    s.part_cap = PART_CAP;
+    s.wide_min = WIDE_MIN;
+    s.ft = 0;
+    s.zero_nnz = 0;
     return s;
 }
 
@@ -447,7 +522,7 @@ static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per
         }                                                                         \
     } while (0)
 
-ias_status Plan::reserve(void **buf, size_t *cap, size_t bytes) {
+ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
     if (*cap >= bytes && *buf) return IAS_SUCCESS;
     if (*buf) HIPC(hipFree(*buf));
     *buf = nullptr;
@@ -460,6 +535,7 @@ ias_status Plan::reserve(void **buf, size_t *cap, size_t bytes) {
 
 ias_plan::~ias_plan() {
     hipSetDevice(device);
+    if (stream) hipStreamSynchronize((hipStream_t)stream);
     for (auto &b : bufs)
         if (b.p) hipFree(b.p);
     for (auto &e : ev)
@@ -468,7 +544,7 @@ ias_plan::~ias_plan() {
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
 }
 
-ias_status Plan::init(int dev, void *strm) {
+ias_status ias_plan::init(int dev, void *strm) {
     device = dev;
     HIPC(hipSetDevice(device));
     if (strm) {
@@ -481,94 +557,121 @@ ias_status Plan::init(int dev, void *strm) {
         own_stream = true;
     }
     for (auto &e : ev) HIPC(hipEventCreate(&e));
-    HIPC(hipHostMalloc(&host_counters, sizeof(Counters)));
+    HIPC(hipHostMalloc(&host_counters, 2 * sizeof(Counters)));
     return IAS_SUCCESS;
 }
 
 template <typename T>
-static T *as(Plan::Buf &b) { return (T *)b.p; }
+static T *as(ias_plan::Buf &b) { return (T *)b.p; }
 
-ias_status Plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
-                          ias_report *rep) {
+ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
+                              ias_report *rep) {
     (void)cols;
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
-    const BinSpec sspec = make_spec(SYM_UPPER, 6);
-    const BinSpec nspec = make_spec(NUM_UPPER, 6);
-    IAS_TRY(reserve(&bufs[B_PROD].p, &bufs[B_PROD].cap, sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(reserve(&bufs[B_NNZ].p, &bufs[B_NNZ].cap, sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(reserve(&bufs[B_SLIST].p, &bufs[B_SLIST].cap, sizeof(int32_t) * rows * MAX_BINS + 4));
-    IAS_TRY(reserve(&bufs[B_NLIST].p, &bufs[B_NLIST].cap, sizeof(int32_t) * rows * MAX_BINS + 4));
-    IAS_TRY(reserve(&bufs[B_SOFF].p, &bufs[B_SOFF].cap, sizeof(int64_t) * (rows + 1)));
-    IAS_TRY(reserve(&bufs[B_NOFF].p, &bufs[B_NOFF].cap, sizeof(int64_t) * (rows + 1)));
-    IAS_TRY(reserve(&bufs[B_CNT].p, &bufs[B_CNT].cap, sizeof(Counters)));
-    IAS_TRY(reserve(&bufs[B_PTR].p, &bufs[B_PTR].cap, sizeof(int64_t) * (rows + 1)));
+    const BinSpec ss = sym_spec(), ns = num_spec();
+    IAS_TRY(reserve(B_PROD, sizeof(int32_t) * (rows + 1)));
+    IAS_TRY(reserve(B_NNZ, sizeof(int32_t) * (rows + 1)));
+    IAS_TRY(reserve(B_SLIST, sizeof(int32_t) * rows * MAX_BINS + 4));
+    IAS_TRY(reserve(B_NLIST, sizeof(int32_t) * rows * MAX_BINS + 4));
+    IAS_TRY(reserve(B_BMOFF, sizeof(int64_t) * (rows + 1)));
+    IAS_TRY(reserve(B_WSOFF, sizeof(int64_t) * (rows + 1)));
+    IAS_TRY(reserve(B_CNT, sizeof(Counters)));
+    IAS_TRY(reserve(B_CNT2, sizeof(Counters)));
+    IAS_TRY(reserve(B_PTR, sizeof(int64_t) * (rows + 1)));
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
-    IAS_TRY(reserve(&bufs[B_PART].p, &bufs[B_PART].cap, sizeof(int64_t) * (nb + 2)));
+    IAS_TRY(reserve(B_PART, sizeof(int64_t) * (nb + 2)));
     Counters *dc = as<Counters>(bufs[B_CNT]);
+    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Counters *hc = (Counters *)host_counters;
 
+    // ---- analysis + binning by products
     HIPC(hipEventRecord(ev[0], s));
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
+    HIPC(hipMemsetAsync(dc2, 0, sizeof(Counters), s));
+    // items worst case: every row partitioned -> sum of ceil(P/cap) <= rows + flops/cap;
+    // bounded below after the counters are read (the kernel writes at most that many).
     if (rows > 0) {
         k_row_products<<<grid_for(rows, AN_BLOCK), AN_BLOCK, 0, s>>>(
             A, B, rows, as<int32_t>(bufs[B_PROD]), &dc->flops, &dc->max_prod);
+        HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        flops = (int64_t)hc->flops;
+        max_prod = hc->max_prod;
+        IAS_TRY(reserve(B_SITEM, sizeof(unsigned long long) * (size_t)(rows + flops / PART_CAP + 2)));
         k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            as<int32_t>(bufs[B_PROD]), rows, sspec, as<int32_t>(bufs[B_SLIST]), dc->sym_count,
-            &dc->sym_ws, as<int64_t>(bufs[B_SOFF]), as<int32_t>(bufs[B_NNZ]));
+            as<int32_t>(bufs[B_PROD]), rows, ss, as<int32_t>(bufs[B_SLIST]),
+            as<unsigned long long>(bufs[B_SITEM]), as<int64_t>(bufs[B_BMOFF]),
+            as<int64_t>(bufs[B_WSOFF]), as<int32_t>(bufs[B_NNZ]), dc);
+    } else {
+        flops = 0;
+        max_prod = 0;
     }
     HIPC(hipEventRecord(ev[1], s));
-    HIPC(hipMemcpyAsync(host_counters, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    Counters hc = *(Counters *)host_counters;
-    flops = (int64_t)hc.flops;
-    max_prod = hc.max_prod;
+    const Counters c1 = *hc;
 
-    // workspace for global-table rows (keys only, 4 B per slot)
-    if (hc.sym_count[sspec.nbins - 1] > 0)
-        IAS_TRY(reserve(&bufs[B_WS].p, &bufs[B_WS].cap, sizeof(int32_t) * hc.sym_ws));
+    // ---- symbolic
     const int32_t *L = as<int32_t>(bufs[B_SLIST]);
     int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
     auto lst = [&](int b) { return L + (int64_t)b * rows; };
+    Bitmap bm{nullptr, nullptr, as<int64_t>(bufs[B_BMOFF])};
+    if (c1.count[ss.nlds + 1] > 0) {
+        IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
+        IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
+        bm.bits = as<uint32_t>(bufs[B_BITS]);
+        bm.pref = as<uint32_t>(bufs[B_BPREF]);
+        HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
+    }
     int c;
-    if ((c = hc.sym_count[1]) > 0)
-        k_symbolic_lds<32, 6, 8><<<grid_for(c, 8), 256, 0, s>>>(A, B, lst(1), c, nnz);
-    if ((c = hc.sym_count[2]) > 0)
-        k_symbolic_lds<64, 8, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, nnz);
-    if ((c = hc.sym_count[3]) > 0)
-        k_symbolic_lds<128, 10, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, nnz);
-    if ((c = hc.sym_count[4]) > 0)
-        k_symbolic_lds<256, 12, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, nnz);
-    if ((c = hc.sym_count[5]) > 0)
-        k_symbolic_lds<512, 14, 1><<<c, 512, 0, s>>>(A, B, lst(5), c, nnz);
-    if ((c = hc.sym_count[6]) > 0)
-        k_symbolic_lds<1024, 15, 1><<<c, 1024, 0, s>>>(A, B, lst(6), c, nnz);
-    if ((c = hc.sym_count[7]) > 0)
-        k_symbolic_global<1024><<<c, 1024, 0, s>>>(A, B, lst(7), as<int64_t>(bufs[B_SOFF]),
-                                                    as<int32_t>(bufs[B_PROD]), c,
-                                                    as<int32_t>(bufs[B_WS]), nnz);
-    // row pointer of C
+    if ((c = c1.count[1]) > 0)
+        k_symbolic_lds<16, 4, 7, 16, 16><<<grid_for(c, 16), 256, 0, s>>>(A, B, lst(1), c, nnz);
+    if ((c = c1.count[2]) > 0)
+        k_symbolic_lds<64, 4, 9, 64, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, nnz);
+    if ((c = c1.count[3]) > 0)
+        k_symbolic_lds<256, 4, 11, 256, 1><<<c, 256, 0, s>>>(A, B, lst(3), c, nnz);
+    if ((c = c1.count[4]) > 0)
+        k_symbolic_lds<512, 4, 12, 256, 1><<<c, 512, 0, s>>>(A, B, lst(4), c, nnz);
+    if ((c = c1.count[5]) > 0)
+        k_symbolic_lds<1024, 4, 13, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(5), c, nnz);
+    if ((c = c1.count[6]) > 0) {
+        k_symbolic_part<512, 4, 13, 256><<<(unsigned)c1.items, 512, 0, s>>>(
+            A, B, as<unsigned long long>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), PART_CAP, bm, nnz,
+            &dc2->overflow);
+        k_bitmap_prefix<<<c, 256, 0, s>>>(lst(6), c, as<int32_t>(bufs[B_PROD]), bm);
+    }
+    HIPC(hipGetLastError());
+
+    // ---- row pointer of C, numeric binning by nnz
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
     if (rows > 0) {
         k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
-                                                          &dc->max_nnz);
+                                                          &dc2->max_nnz);
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART]), nb);
-        k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
-                                                         ptr);
+        k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
+        IAS_TRY(reserve(B_NITEM, sizeof(unsigned long long) * (size_t)(rows + flops / PART_CAP + 2)));
         k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            nnz, rows, nspec, as<int32_t>(bufs[B_NLIST]), dc->num_count, &dc->num_ws,
-            as<int64_t>(bufs[B_NOFF]), nullptr);
+            nnz, rows, ns, as<int32_t>(bufs[B_NLIST]), as<unsigned long long>(bufs[B_NITEM]), nullptr,
+            as<int64_t>(bufs[B_WSOFF]), nullptr, dc2);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
     }
+    HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[2], s));
-    HIPC(hipMemcpyAsync(host_counters, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipMemcpyAsync(&nnz_total, ptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    hc = *(Counters *)host_counters;
-    std::copy(hc.num_count, hc.num_count + MAX_BINS, num_count);
-    num_ws = hc.num_ws;
-    max_nnz = hc.max_nnz;
+    const Counters c2 = hc[1];
+    if (c2.overflow) {
+        set_last_error("hash partition table overflow in the symbolic pass");
+        return IAS_ERROR_OVERFLOW;
+    }
+    std::copy(c2.count, c2.count + MAX_BINS, num_count);
+    num_items = c2.items;
+    num_ws = c2.ws_slots;
+    max_nnz = c2.max_nnz;
     if (rep) {
         float a = 0, b = 0;
         hipEventElapsedTime(&a, ev[0], ev[1]);
@@ -583,36 +686,52 @@ ias_status Plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t co
     return IAS_SUCCESS;
 }
 
-ias_status Plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_report *rep) {
+ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_report *rep) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     const int64_t rows = n_rows;
-    const int nglob = MAX_BIN_LDS + 1;
-    if (num_count[nglob] > 0) IAS_TRY(reserve(&bufs[B_WS].p, &bufs[B_WS].cap, 20ull * num_ws));
+    const BinSpec ns = num_spec();
+    const int part_bin = ns.nlds + 1, wide_bin = ns.nlds + 2;
+    if (num_count[wide_bin] > 0) IAS_TRY(reserve(B_WS, 20ull * num_ws));
     const int32_t *L = as<int32_t>(bufs[B_NLIST]);
     auto lst = [&](int b) { return L + (int64_t)b * rows; };
+    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     HIPC(hipEventRecord(ev[3], s));
     int c;
     if ((c = num_count[1]) > 0)
-        k_numeric_lds<32, 5, 8><<<grid_for(c, 8), 256, 0, s>>>(A, B, lst(1), c, out);
+        k_numeric_lds<16, 4, 5, 16, 16><<<grid_for(c, 16), 256, 0, s>>>(A, B, lst(1), c, out);
     if ((c = num_count[2]) > 0)
-        k_numeric_lds<64, 7, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, out);
+        k_numeric_lds<32, 4, 7, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(A, B, lst(2), c, out);
     if ((c = num_count[3]) > 0)
-        k_numeric_lds<128, 9, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, out);
+        k_numeric_lds<128, 4, 9, 128, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, out);
     if ((c = num_count[4]) > 0)
-        k_numeric_lds<256, 11, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, out);
+        k_numeric_lds<512, 4, 11, 256, 1><<<c, 512, 0, s>>>(A, B, lst(4), c, out);
     if ((c = num_count[5]) > 0)
-        k_numeric_lds<512, 12, 1><<<c, 512, 0, s>>>(A, B, lst(5), c, out);
+        k_numeric_lds<1024, 2, 12, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(5), c, out);
     if ((c = num_count[6]) > 0)
-        k_numeric_lds<1024, 13, 1><<<c, 1024, 0, s>>>(A, B, lst(6), c, out);
-    if ((c = num_count[nglob]) > 0)
-        k_numeric_global<1024><<<c, 1024, 0, s>>>(A, B, lst(nglob), as<int64_t>(bufs[B_NOFF]),
-                                                   as<int32_t>(bufs[B_NNZ]), c,
-                                                   (char *)bufs[B_WS].p, out);
+        k_numeric_lds<1024, 2, 13, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(6), c, out);
+    if (num_count[part_bin] > 0)
+        k_numeric_part<1024, 2, 13, 256><<<(unsigned)num_items, 1024, 0, s>>>(
+            A, B, as<unsigned long long>(bufs[B_NITEM]), as<int32_t>(bufs[B_NNZ]), PART_CAP, bm, out,
+            &dc2->overflow);
+    if ((c = num_count[wide_bin]) > 0)
+        k_numeric_global<1024, 2, 256><<<c, 1024, 0, s>>>(A, B, lst(wide_bin), as<int64_t>(bufs[B_WSOFF]),
+                                                          as<int32_t>(bufs[B_NNZ]), c,
+                                                          (char *)bufs[B_WS].p, out);
     if (out.row_idx && rows > 0)
         k_fill_rows<<<grid_for(rows * WAVE, 256), 256, 0, s>>>(out.ptr, rows, out.row_idx);
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[4], s));
+    if (num_count[part_bin] > 0) {
+        int32_t of = 0;
+        HIPC(hipMemcpyAsync(&of, &dc2->overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        if (of) {
+            set_last_error("hash partition table overflow in the numeric pass");
+            return IAS_ERROR_OVERFLOW;
+        }
+    }
     if (rep) {
         HIPC(hipEventSynchronize(ev[4]));
         float a = 0, t = 0;
@@ -624,30 +743,16 @@ ias_status Plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_repor
     return IAS_SUCCESS;
 }
 
-ias_status Plan::shift(int64_t *p, int64_t n, int64_t off) {
-    if (n <= 0 || off == 0) return IAS_SUCCESS;
-    k_shift<<<grid_for(n, 256), 256, 0, (hipStream_t)stream>>>(p, n, off);
-    HIPC(hipGetLastError());
-    return IAS_SUCCESS;
-}
-
-
 // ------------------------------------------------------------------ row sort host
-static const int SORT_UPPER[] = {0, 32, 128, 512, 2048, 4096, 8192};
-
 static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32_t *len_in,
                                  int64_t stride, int64_t rows, int32_t *col, double *val) {
     if (rows <= 0) return IAS_SUCCESS;
     hipStream_t s = (hipStream_t)plan->stream;
     HIPC(hipSetDevice(plan->device));
-    IAS_TRY(plan->reserve(&plan->bufs[ias_plan::B_TMP0].p, &plan->bufs[ias_plan::B_TMP0].cap,
-                          sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(plan->reserve(&plan->bufs[ias_plan::B_TMP1].p, &plan->bufs[ias_plan::B_TMP1].cap,
-                          sizeof(int32_t) * rows * MAX_BINS + 4));
-    IAS_TRY(plan->reserve(&plan->bufs[ias_plan::B_TMP2].p, &plan->bufs[ias_plan::B_TMP2].cap,
-                          sizeof(int64_t) * (rows + 1)));
-    IAS_TRY(plan->reserve(&plan->bufs[ias_plan::B_TMP3].p, &plan->bufs[ias_plan::B_TMP3].cap,
-                          sizeof(Counters)));
+    IAS_TRY(plan->reserve(ias_plan::B_TMP0, sizeof(int32_t) * (rows + 1)));
+    IAS_TRY(plan->reserve(ias_plan::B_TMP1, sizeof(int32_t) * rows * MAX_BINS + 4));
+    IAS_TRY(plan->reserve(ias_plan::B_TMP2, sizeof(int64_t) * (rows + 1)));
+    IAS_TRY(plan->reserve(ias_plan::B_TMP3, sizeof(Counters)));
     const int32_t *len = len_in;
     if (ptr) {
         k_row_len<<<grid_for(rows, 256), 256, 0, s>>>(ptr, rows, (int32_t *)plan->bufs[ias_plan::B_TMP0].p);
@@ -655,33 +760,38 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     }
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
-    const BinSpec spec = make_spec(SORT_UPPER, 6);
+    BinSpec spec{};
+    spec.nlds = 6;
+    const int32_t u[] = {0, 32, 128, 512, 2048, 4096, 8192};
+    for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
+    spec.part_cap = 1;
+    spec.wide_min = 8193;   // everything beyond the LDS bins -> global workspace
     int32_t *lists = (int32_t *)plan->bufs[ias_plan::B_TMP1].p;
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
-    k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, rows, spec, lists, dc->num_count,
-                                                                &dc->num_ws, offs, nullptr);
+    k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, rows, spec, lists, nullptr, nullptr,
+                                                                offs, nullptr, dc);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    if (hc.num_count[7] > 0)
-        IAS_TRY(plan->reserve(&plan->bufs[ias_plan::B_TMP4].p, &plan->bufs[ias_plan::B_TMP4].cap,
-                              12ull * hc.num_ws + 16));
+    const int wide = spec.nlds + 2;
+    if (hc.count[wide] > 0)
+        IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     auto lst = [&](int b) { return lists + (int64_t)b * rows; };
     int c;
-    if ((c = hc.num_count[1]) > 0)
+    if ((c = hc.count[1]) > 0)
         k_sort_lds<32, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[2]) > 0)
+    if ((c = hc.count[2]) > 0)
         k_sort_lds<64, 128, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(2), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[3]) > 0)
+    if ((c = hc.count[3]) > 0)
         k_sort_lds<256, 512, 1><<<c, 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[4]) > 0)
+    if ((c = hc.count[4]) > 0)
         k_sort_lds<512, 2048, 1><<<c, 512, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[5]) > 0)
+    if ((c = hc.count[5]) > 0)
         k_sort_lds<1024, 4096, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[6]) > 0)
+    if ((c = hc.count[6]) > 0)
         k_sort_lds<1024, 8192, 1><<<c, 1024, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
-    if ((c = hc.num_count[7]) > 0)
-        k_sort_global<<<c, 1024, 0, s>>>(lst(7), c, offs, ptr, len, stride, col, val,
+    if ((c = hc.count[wide]) > 0)
+        k_sort_global<<<c, 1024, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val,
                                          (char *)plan->bufs[ias_plan::B_TMP4].p);
     HIPC(hipGetLastError());
     return IAS_SUCCESS;

@@ -8,29 +8,40 @@
 
 namespace ias {
 
-constexpr int MAX_BINS = 8;      // 0 = empty rows, 1..6 = LDS bins, 7 = global table
-constexpr int MAX_BIN_LDS = 6;
+constexpr int MAX_BINS = 10;   // 0 = empty rows, 1..nlds = LDS bins, nlds+1 = hash
+                               // partitions, nlds+2 = global-memory table
 
+// How a pass bins its rows by `key` (products or nnz).
 struct BinSpec {
-    int32_t nbins;
+    int32_t nlds;              // LDS bins 1..nlds cover key <= upper[nlds]
     int32_t upper[MAX_BINS];
+    int32_t part_cap;          // keys per hash partition in bin nlds+1
+    int32_t wide_min;          // key >= wide_min -> bin nlds+2 (0: never)
+    int32_t ft;                // give partitioned rows a first-touch bitmap
+    int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
 };
 
-// Device-side counters, copied to the host after binning and after the scan.
+// Device-side counters, copied to the host after each binning.
 struct Counters {
     unsigned long long flops;
-    unsigned long long sym_ws;      // global-table slots needed by symbolic rows
-    unsigned long long num_ws;      // global-table slots needed by numeric rows
+    unsigned long long items;     // (row, partition) work items
+    unsigned long long bm_words;  // first-touch bitmap words
+    unsigned long long ws_slots;  // global-table slots
     int32_t max_prod;
     int32_t max_nnz;
-    int32_t sym_count[MAX_BINS];
-    int32_t num_count[MAX_BINS];
+    int32_t overflow;
+    int32_t pad;
+    int32_t count[MAX_BINS];
 };
 
 }  // namespace ias
 
 struct ias_plan {
-    enum { B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SOFF, B_NOFF, B_CNT, B_PTR, B_PART, B_WS, B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5, B_COUNT };
+    enum {
+        B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
+        B_CNT, B_CNT2, B_PTR, B_PART, B_WS,
+        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
+    };
     struct Buf {
         void *p = nullptr;
         size_t cap = 0;
@@ -49,6 +60,7 @@ struct ias_plan {
     int32_t max_prod = 0;
     int32_t max_nnz = 0;
     int32_t num_count[ias::MAX_BINS] = {};
+    unsigned long long num_items = 0;
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;
@@ -56,11 +68,11 @@ struct ias_plan {
     ~ias_plan();
     ias_status init(int device, void *stream);
     ias_status reserve(void **buf, size_t *cap, size_t bytes);
+    ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                         int64_t cols, ias_report *rep);
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
-    ias_status shift(int64_t *p, int64_t n, int64_t off);
 };
 
 namespace ias {

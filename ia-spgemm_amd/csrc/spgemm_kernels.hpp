@@ -3,22 +3,24 @@
 // Algorithm (Gustavson row-wise, C(i,:) = sum_j A(i,j) * B(j,:)), restating
 // CSR_MUL_CSR (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:85-193) so that
 // the output is value-for-value identical to it:
-//   * pass 1 (symbolic): distinct output columns per row, counted in a
-//     per-row open-addressing hash table (keys only) held in LDS;
-//   * pass 2 (numeric): the same hash, now carrying a value and the
-//     first-touch ("discovery") rank of every column.  Products of a row are
-//     processed in the reference's order p = 0..P-1 (A entries in row order,
-//     then B entries in row order), P consecutive products per step, one per
-//     lane.  Lanes whose products hit the same column inside a step are
-//     serialised in lane order (owner = atomicMin), so every sum is formed as
-//     the reference forms it: s = 0.0 + p0, s = s + p1, ... (no FMA: the file
-//     is compiled with -ffp-contract=off).  A column's rank is the number of
-//     distinct columns discovered before it; it is placed at nnz-1-rank
-//     (reverse first-touch, the reference's linked-list order) or at rank
-//     (forward first-touch, COO_MUL_COO's order).
-// Rows are binned by work (products for pass 1, nnz for pass 2); each bin has
-// a team size (32..1024 lanes) and an LDS table size; rows beyond the LDS
-// capacity use the same code on a per-row table in global memory.
+//   * symbolic: distinct output columns per row, counted in a per-row
+//     open-addressing hash table (keys only) held in LDS;
+//   * numeric: the same hash, now carrying a value and the first-touch
+//     ("discovery") rank of every column.  The products of a row are taken in
+//     the reference's order p = 0..P-1 (A entries in row order, then B entries
+//     in row order), TEAM*K of them per step, K per lane.  Items of a step that
+//     hit the same column are serialised in product order (owner =
+//     atomicMin of the item id), so every sum is formed as the reference forms
+//     it: s = 0.0 + p0, s = s + p1, ... (no FMA: -ffp-contract=off).  A column's
+//     rank is the number of distinct columns discovered before it; the entry
+//     lands at nnz-1-rank (reverse first-touch, the reference's linked-list
+//     order) or at rank (forward first-touch, COO_MUL_COO's order).
+// Rows are binned by work (products for symbolic, nnz for numeric); each bin
+// has a team size (16..1024 lanes) and an LDS table.  Rows too large for one
+// LDS table are split by a hash of the column into `nparts` partitions, one
+// workgroup each; the symbolic pass then also records, per row, a bitmap of
+// first-touch product positions (and its word prefix counts) from which a
+// partition computes the global discovery rank of its columns.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -61,6 +63,15 @@ struct Out {
     __device__ __forceinline__ int64_t start(int64_t i) const { return ptr ? ptr[i] : i * stride; }
 };
 
+// First-touch bitmap of the partitioned rows (written by the symbolic pass):
+// row r owns words [off[r], off[r] + ceil(P/32)) of `bits`, and `pref` holds
+// the exclusive prefix popcount of those words.
+struct Bitmap {
+    uint32_t *bits;
+    uint32_t *pref;
+    const int64_t *off;   // per row, in words
+};
+
 // ---------------------------------------------------------------- team ops
 // A team is TEAM consecutive lanes.  TEAM <= 64: several teams per wave,
 // synchronised at wave level.  TEAM > 64: exactly one team per workgroup.
@@ -87,30 +98,6 @@ struct Team {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-    // Exclusive count of `flag` over the team in lane order; `total` = team count.
-    __device__ __forceinline__ static int excl_count(bool flag, int &total, int *scratch) {
-        const uint64_t b = __ballot(flag);
-        const uint64_t lt = (1ull << __lane_id()) - 1ull;
-        if constexpr (!MULTI) {
-            const uint64_t m = b & mask();
-            total = __popcll(m);
-            return __popcll(m & lt);
-        } else {
-            const int w = threadIdx.x / WAVE;
-            if ((threadIdx.x & (WAVE - 1)) == 0) scratch[w] = __popcll(b);
-            __syncthreads();
-            int before = 0, tot = 0;
-#pragma unroll
-            for (int i = 0; i < NWAVES; ++i) {
-                const int c = scratch[i];
-                before += (i < w) ? c : 0;
-                tot += c;
-            }
-            __syncthreads();
-            total = tot;
-            return before + __popcll(b & lt);
         }
     }
     // Exclusive prefix sum of v over the team; `total` = team sum.
@@ -142,6 +129,48 @@ struct Team {
             return before + x - v;
         }
     }
+    // Exclusive count of K flags per lane in item order (item id = k*TEAM +
+    // lane, k-major); rank[k] gets each item's count, returns the team total.
+    template <int K>
+    __device__ __forceinline__ static int excl_count_items(const bool (&f)[K], int (&rank)[K],
+                                                           int *scratch) {
+        const uint64_t lt = (1ull << __lane_id()) - 1ull;
+        uint64_t b[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) b[k] = __ballot(f[k]);
+        if constexpr (!MULTI) {
+            const uint64_t m = mask();
+            int run = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                rank[k] = run + __popcll(b[k] & m & lt);
+                run += __popcll(b[k] & m);
+            }
+            return run;
+        } else {
+            const int w = threadIdx.x / WAVE;
+            if ((threadIdx.x & (WAVE - 1)) == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) scratch[w * K + k] = __popcll(b[k]);
+            }
+            __syncthreads();
+            int run = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                int before = 0, tot = 0;
+#pragma unroll
+                for (int i = 0; i < NWAVES; ++i) {
+                    const int c = scratch[i * K + k];
+                    before += (i < w) ? c : 0;
+                    tot += c;
+                }
+                rank[k] = run + before + __popcll(b[k] & lt);
+                run += tot;
+            }
+            __syncthreads();
+            return run;
+        }
+    }
     __device__ __forceinline__ static bool any(bool p) {
         if constexpr (MULTI) return __syncthreads_or(p) != 0;
         else return (__ballot(p) & mask()) != 0ull;
@@ -153,39 +182,50 @@ struct Team {
     }
 };
 
-__device__ __forceinline__ uint32_t hash_col(int32_t c) { return (uint32_t)c * 0x9E3779B1u; }
+// table slot hash and (independent) partition hash
+__device__ __forceinline__ uint32_t slot_hash(int32_t c, uint32_t log2s) {
+    return log2s ? (((uint32_t)c * 0x9E3779B1u) >> (32u - log2s)) : 0u;
+}
+__device__ __forceinline__ uint32_t part_of(int32_t c, uint32_t nparts) {
+    const uint32_t h = ((uint32_t)c * 0x85EBCA6Bu) ^ ((uint32_t)c >> 16);
+    return (uint32_t)(((uint64_t)(h * 0xC2B2AE35u) * nparts) >> 32);
+}
 
 // ---------------------------------------------------------------- tables
-// Keys-only table (symbolic).  `log2s` is the table's log2 size.
-struct KeyTable {
+// Keys (+ optional first-touch position) table of the symbolic pass.
+// insert returns 1 when it created the key, 0 when present, -1 when the
+// table is full (only possible for hash partitions; the caller flags it).
+template <bool FT>
+struct SymTable {
     int32_t *key;
+    uint32_t *minp;   // FT only
     uint32_t log2s;
-    __device__ __forceinline__ uint32_t first(int32_t c) const {
-        return log2s ? (hash_col(c) >> (32u - log2s)) : 0u;
-    }
-    // Returns true when this call inserted the key.
-    __device__ __forceinline__ bool insert(int32_t c) const {
+    __device__ __forceinline__ int insert(int32_t c, uint32_t p) const {
         const uint32_t m = (1u << log2s) - 1u;
-        uint32_t s = first(c);
-        while (true) {
+        uint32_t s = slot_hash(c, log2s);
+        for (uint32_t probe = 0; probe <= m; ++probe) {
             const int32_t prev = atomicCAS(&key[s], EMPTY_KEY, c);
-            if (prev == EMPTY_KEY) return true;
-            if (prev == c) return false;
+            if (prev == EMPTY_KEY || prev == c) {
+                if constexpr (FT) atomicMin(&minp[s], p);
+                return prev == EMPTY_KEY ? 1 : 0;
+            }
             s = (s + 1u) & m;
         }
+        return -1;
     }
 };
 
-// Numeric table, LDS flavour: meta = rank << 12 | owner (owner 0xFFF = none,
-// rank 0xFFFFF = not yet discovered).  Global flavour: 64-bit meta, rank << 32 | owner.
+// Numeric table, LDS flavour: meta = rank << 13 | owner (owner 0x1FFF = none,
+// rank 0x7FFFF = not yet discovered).  Global flavour (rows beyond 2^19 nnz):
+// 64-bit meta, rank << 32 | owner.
 template <bool WIDE>
 struct MetaTraits;
 template <>
 struct MetaTraits<false> {
     using T = uint32_t;
-    static constexpr int SHIFT = 12;
-    static constexpr T OWN = 0xFFFu;
-    static constexpr T RANK_NONE = 0xFFFFFu;
+    static constexpr int SHIFT = 13;
+    static constexpr T OWN = 0x1FFFu;
+    static constexpr T RANK_NONE = 0x7FFFFu;
     static constexpr T INIT = 0xFFFFFFFFu;
 };
 template <>
@@ -206,18 +246,19 @@ struct NumTable {
     double *val;
     uint32_t log2s;
 
-    __device__ __forceinline__ uint32_t find_or_insert(int32_t c) const {
+    __device__ __forceinline__ int find_or_insert(int32_t c) const {
         const uint32_t m = (1u << log2s) - 1u;
-        uint32_t s = log2s ? (hash_col(c) >> (32u - log2s)) : 0u;
-        while (true) {
+        uint32_t s = slot_hash(c, log2s);
+        for (uint32_t probe = 0; probe <= m; ++probe) {
             const int32_t prev = atomicCAS(&key[s], EMPTY_KEY, c);
-            if (prev == EMPTY_KEY || prev == c) return s;
+            if (prev == EMPTY_KEY || prev == c) return (int)s;
             s = (s + 1u) & m;
         }
+        return -1;
     }
-    __device__ __forceinline__ void claim(uint32_t s, int lane) const {
+    __device__ __forceinline__ void claim(uint32_t s, uint32_t id) const {
         const M cur = __hip_atomic_load(&meta[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        atomicMin(&meta[s], (cur & ~MT::OWN) | (M)lane);
+        atomicMin(&meta[s], (cur & ~MT::OWN) | (M)id);
     }
     __device__ __forceinline__ M load(uint32_t s) const {
         return __hip_atomic_load(&meta[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -225,13 +266,13 @@ struct NumTable {
 };
 
 // ---------------------------------------------------------------- segment
-// The A entries of the row currently being expanded, staged in LDS:
-// bstart = start of B row, aval = A value, pref = exclusive prefix of B row lengths.
-template <int TEAM, bool NUMERIC>
+// Up to SEG A entries of the row being expanded, staged in LDS: bstart =
+// start of the B row, aval = A value, pref = exclusive prefix of B row lengths.
+template <int SEG, bool NUMERIC>
 struct Seg {
-    int64_t bstart[TEAM];
-    int32_t pref[TEAM];
-    double aval[NUMERIC ? TEAM : 1];
+    int64_t bstart[SEG];
+    int32_t pref[SEG];
+    double aval[NUMERIC ? SEG : 1];
 };
 
 // Largest jj in [0, n) with pref[jj] <= p (pref[0] == 0 <= p).
@@ -245,15 +286,16 @@ __device__ __forceinline__ int seg_find(const int32_t *pref, int n, int p) {
     return lo;
 }
 
-// Load segment [seg0, seg0+TEAM) of A row (as, an) into LDS; returns the
-// number of products of the segment (team-uniform).
-template <int TEAM, bool NUMERIC>
+// Stage A entries [seg0, seg0 + SEG) of row (as, an); returns the products of
+// the segment (team-uniform).  Requires SEG <= TEAM.
+template <int TEAM, int SEG, bool NUMERIC>
 __device__ __forceinline__ int load_segment(const Rows &A, const Rows &B, int64_t as, int32_t an,
-                                            int32_t seg0, Seg<TEAM, NUMERIC> &sg, int *scratch,
+                                            int32_t seg0, Seg<SEG, NUMERIC> &sg, int *scratch,
                                             int &nseg) {
+    static_assert(SEG <= TEAM, "segment loads one entry per lane");
     using TM = Team<TEAM>;
     const int lane = TM::lane();
-    nseg = min(TEAM, an - seg0);
+    nseg = min(SEG, an - seg0);
     int blen = 0;
     if (lane < nseg) {
         const int64_t e = as + seg0 + lane;
@@ -273,44 +315,84 @@ __device__ __forceinline__ int load_segment(const Rows &A, const Rows &B, int64_
 }
 
 // ---------------------------------------------------------------- symbolic
-// One team counts the distinct columns of one row into `table`.
-template <int TEAM>
+// One team counts the distinct columns of one row (or of one hash partition
+// of it when nparts > 1).  FT: also the first-touch position of every column,
+// published as bits of the row's bitmap.  Returns the team's count; *overflow
+// is set when a partition table filled up.
+template <int TEAM, int K, int SEG, bool FT>
 __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, int64_t row,
-                                                const KeyTable &table, Seg<TEAM, false> &sg,
-                                                int *scratch) {
+                                                const SymTable<FT> &table, uint32_t part,
+                                                uint32_t nparts, Seg<SEG, false> &sg,
+                                                int *scratch, uint32_t *bits, int *overflow) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = 1u << table.log2s;
-    for (uint32_t s = lane; s < S; s += TEAM) table.key[s] = EMPTY_KEY;
+    for (uint32_t s = lane; s < S; s += TEAM) {
+        table.key[s] = EMPTY_KEY;
+        if constexpr (FT) table.minp[s] = 0xFFFFFFFFu;
+    }
     TM::sync();
     int64_t as = 0;
     int32_t an = 0;
     if (row >= 0) A.row(row, as, an);
     int created = 0;
-    for (int32_t seg0 = 0; seg0 < an; seg0 += TEAM) {
+    bool full = false;
+    uint32_t pbase = 0;
+    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
         int nseg;
-        const int P = load_segment<TEAM, false>(A, B, as, an, seg0, sg, scratch, nseg);
-        for (int p0 = 0; p0 < P; p0 += TEAM) {
-            const int p = p0 + lane;
-            if (p < P) {
-                const int jj = seg_find(sg.pref, nseg, p);
-                const int64_t kk = sg.bstart[jj] + (p - sg.pref[jj]);
-                created += table.insert(B.col[kk]) ? 1 : 0;
+        const int P = load_segment<TEAM, SEG, false>(A, B, as, an, seg0, sg, scratch, nseg);
+        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+            int32_t c[K];
+            bool v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int p = p0 + k * TEAM + lane;
+                v[k] = p < P;
+                if (v[k]) {
+                    const int jj = seg_find(sg.pref, nseg, p);
+                    c[k] = B.col[sg.bstart[jj] + (p - sg.pref[jj])];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (v[k] && (nparts <= 1 || part_of(c[k], nparts) == part)) {
+                    const int r = table.insert(c[k], pbase + p0 + k * TEAM + lane);
+                    created += r > 0 ? 1 : 0;
+                    full |= r < 0;
+                }
             }
         }
+        pbase += (uint32_t)P;
         TM::sync();
     }
+    if constexpr (FT) {
+        for (uint32_t s = lane; s < S; s += TEAM)
+            if (table.key[s] != EMPTY_KEY) {
+                const uint32_t p = table.minp[s];
+                atomicOr(&bits[p >> 5], 1u << (p & 31));
+            }
+    }
+    if (full) atomicOr(overflow, 1);
     return TM::sum(created, scratch);
 }
 
 // ---------------------------------------------------------------- numeric
-template <int TEAM, bool WIDE>
+// PART == false: the whole row in one LDS table, ranks from team scans,
+// emission staged through LDS so C is written with coalesced stores.
+// PART == true : hash partition `part` of the row; ranks from the symbolic
+// first-touch bitmap; entries stored straight to their final positions.
+template <int TEAM, int K, int SEG, bool WIDE, bool PART, int PER>
 __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_t row,
-                                            const NumTable<WIDE> &t, Seg<TEAM, true> &sg,
-                                            int *scratch, const Out &out) {
+                                            const NumTable<WIDE> &t, uint32_t part,
+                                            uint32_t nparts, const uint32_t *bits,
+                                            const uint32_t *bpref, Seg<SEG, true> &sg,
+                                            int *scratch, const Out &out, int32_t nnz_row,
+                                            int *overflow) {
     using TM = Team<TEAM>;
     using MT = MetaTraits<WIDE>;
     using M = typename MT::T;
+    static_assert((unsigned long long)TEAM * K < (unsigned long long)MT::OWN,
+                  "item ids must fit the owner field");
     const int lane = TM::lane();
     const uint32_t S = 1u << t.log2s;
     for (uint32_t s = lane; s < S; s += TEAM) {
@@ -322,65 +404,154 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
     int32_t an = 0;
     if (row >= 0) A.row(row, as, an);
     uint32_t base_rank = 0;
-    for (int32_t seg0 = 0; seg0 < an; seg0 += TEAM) {
+    uint32_t pbase = 0;
+    bool full = false;
+    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
         int nseg;
-        const int P = load_segment<TEAM, true>(A, B, as, an, seg0, sg, scratch, nseg);
-        for (int p0 = 0; p0 < P; p0 += TEAM) {
-            const int p = p0 + lane;
-            bool pending = p < P;
-            uint32_t slot = 0;
-            double prod = 0.0;
-            if (pending) {
-                const int jj = seg_find(sg.pref, nseg, p);
-                const int64_t kk = sg.bstart[jj] + (p - sg.pref[jj]);
-                const int32_t c = B.col[kk];
-                prod = sg.aval[jj] * B.val[kk];
-                slot = t.find_or_insert(c);
+        const int P = load_segment<TEAM, SEG, true>(A, B, as, an, seg0, sg, scratch, nseg);
+        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+            int slot[K];
+            double prod[K];
+            bool pend[K];
+            int32_t c[K];
+            int jj[K];
+            int64_t kk[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int p = p0 + k * TEAM + lane;
+                pend[k] = p < P;
+                if (pend[k]) {
+                    jj[k] = seg_find(sg.pref, nseg, p);
+                    kk[k] = sg.bstart[jj[k]] + (p - sg.pref[jj[k]]);
+                    c[k] = B.col[kk[k]];
+                }
+            }
+            if constexpr (PART) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) pend[k] = pend[k] && part_of(c[k], nparts) == part;
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (pend[k]) prod[k] = sg.aval[jj[k]] * B.val[kk[k]];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                slot[k] = 0;
+                if (pend[k]) {
+                    const int s = t.find_or_insert(c[k]);
+                    if (s < 0) {
+                        full = true;
+                        pend[k] = false;
+                    } else {
+                        slot[k] = s;
+                    }
+                }
             }
             bool first_round = true;
             while (true) {
-                if (pending) t.claim(slot, lane);
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (pend[k]) t.claim((uint32_t)slot[k], (uint32_t)(k * TEAM + lane));
                 TM::sync();
-                M m = pending ? t.load(slot) : (M)0;
-                const bool win = pending && ((m & MT::OWN) == (M)lane);
-                M rank = m >> MT::SHIFT;
+                bool win[K];
+                M rank[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const M m = pend[k] ? t.load((uint32_t)slot[k]) : (M)0;
+                    win[k] = pend[k] && ((m & MT::OWN) == (M)(k * TEAM + lane));
+                    rank[k] = m >> MT::SHIFT;
+                }
                 if (first_round) {
-                    const bool ft = win && rank == MT::RANK_NONE;
-                    int total;
-                    const int r = TM::excl_count(ft, total, scratch);
-                    if (ft) rank = (M)(base_rank + (uint32_t)r);
-                    base_rank += (uint32_t)total;
-                    if (win) {
-                        const double v = ft ? (out.first_assign ? prod : 0.0 + prod)
-                                            : t.val[slot] + prod;
-                        t.val[slot] = v;
+                    bool ft[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) ft[k] = win[k] && rank[k] == MT::RANK_NONE;
+                    if constexpr (!PART) {
+                        int r[K];
+                        const int total = TM::template excl_count_items<K>(ft, r, scratch);
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            if (ft[k]) rank[k] = (M)(base_rank + (uint32_t)r[k]);
+                        base_rank += (uint32_t)total;
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < K; ++k)
+                            if (ft[k]) {
+                                const uint32_t p = pbase + (uint32_t)(p0 + k * TEAM + lane);
+                                rank[k] = (M)(bpref[p >> 5] + __popc(bits[p >> 5] & ((1u << (p & 31)) - 1u)));
+                            }
                     }
-                } else if (win) {
-                    t.val[slot] = t.val[slot] + prod;
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (win[k]) {
+                            const double v = ft[k] ? (out.first_assign ? prod[k] : 0.0 + prod[k])
+                                                   : t.val[slot[k]] + prod[k];
+                            t.val[slot[k]] = v;
+                        }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (win[k]) t.val[slot[k]] = t.val[slot[k]] + prod[k];
                 }
-                if (win) {
-                    t.meta[slot] = (rank << MT::SHIFT) | MT::OWN;
-                    pending = false;
-                }
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (win[k]) {
+                        t.meta[slot[k]] = (rank[k] << MT::SHIFT) | MT::OWN;
+                        pend[k] = false;
+                    }
                 first_round = false;
+                bool any_pend = false;
+#pragma unroll
+                for (int k = 0; k < K; ++k) any_pend |= pend[k];
                 if constexpr (!TM::MULTI) TM::sync();
-                if (!TM::any(pending)) break;
+                if (!TM::any(any_pend)) break;
+            }
+        }
+        pbase += (uint32_t)P;
+        TM::sync();
+    }
+    if (full) atomicOr(overflow, 1);
+    if (row < 0) return;
+    const int64_t o = out.start(row);
+    if constexpr (PART || WIDE) {
+        const uint32_t nnz = PART ? (uint32_t)nnz_row : base_rank;
+        for (uint32_t s = lane; s < S; s += TEAM) {
+            const int32_t cc = t.key[s];
+            if (cc != EMPTY_KEY) {
+                const uint32_t r = (uint32_t)(t.meta[s] >> MT::SHIFT);
+                const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
+                out.col[pos] = cc;
+                out.val[pos] = t.val[s];
+                if (out.row_idx) out.row_idx[pos] = (int32_t)row;
+            }
+        }
+    } else {
+        // LDS-staged emission: slots -> registers -> (col, val) at their final
+        // position in the key/val arrays -> coalesced stores of the row.
+        // PER = S / TEAM slots per lane (compile-time, from the kernel).
+        const uint32_t nnz = base_rank;
+        int32_t kc[PER];
+        uint32_t kr[PER];
+        double kv[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const uint32_t s = (uint32_t)i * TEAM + lane;
+            kc[i] = t.key[s];
+            kr[i] = (uint32_t)(t.meta[s] >> MT::SHIFT);
+            kv[i] = t.val[s];
+        }
+        TM::sync();
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            if (kc[i] != EMPTY_KEY) {
+                const uint32_t pos = out.order == 0 ? nnz - 1u - kr[i] : kr[i];
+                t.key[pos] = kc[i];
+                t.val[pos] = kv[i];
             }
         }
         TM::sync();
-    }
-    if (row < 0) return;
-    // emit
-    const int64_t o = out.start(row);
-    const uint32_t nnz = base_rank;
-    for (uint32_t s = lane; s < S; s += TEAM) {
-        const int32_t c = t.key[s];
-        if (c != EMPTY_KEY) {
-            const uint32_t r = (uint32_t)(t.meta[s] >> MT::SHIFT);
-            const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
-            out.col[pos] = c;
-            out.val[pos] = t.val[s];
-            if (out.row_idx) out.row_idx[pos] = (int32_t)row;
+        for (uint32_t e = lane; e < nnz; e += TEAM) {
+            out.col[o + e] = t.key[e];
+            out.val[o + e] = t.val[e];
+            if (out.row_idx) out.row_idx[o + e] = (int32_t)row;
         }
     }
 }

@@ -129,6 +129,54 @@ def test_csr_long_rows_global_tables():
     assert_csr_identical(got, ref, "long rows")
 
 
+def wide_row(n=1 << 20, head=1000, per=600):
+    """Row 0 reaches head*per = 600k distinct columns: beyond the 19-bit rank
+    field of the LDS/partition tables, so the 64-bit global-table path runs."""
+    rp = np.zeros(n + 1, np.int64)
+    lens = np.zeros(n, np.int64)
+    lens[0] = head
+    lens[1:head] = per
+    rp[1:] = np.cumsum(lens)
+    col = [np.arange(head)] + [np.arange(i * head, i * head + per) for i in range(1, head)]
+    col = np.concatenate(col).astype(np.int32)
+    val = ((np.arange(col.size) % 7) + 1).astype(np.float64)
+    return ias.HostCsr(n, n, rp, col, val)
+
+
+def heavy_collisions(n=4096, head=3000, per=10, seed=3):
+    """Row 0: 30k products onto 10 columns (long ordered sums in one LDS slot);
+    symbolic takes the hash-partition path (P > 5460), numeric the smallest bin."""
+    rng = np.random.default_rng(seed)
+    rp = np.zeros(n + 1, np.int64)
+    lens = np.full(n, per, np.int64)
+    lens[0] = head
+    rp[1:] = np.cumsum(lens)
+    col = np.concatenate([rng.choice(np.arange(1, n), head, replace=False)] +
+                         [np.arange(per)] * (n - 1)).astype(np.int32)
+    val = rng.uniform(-1, 1, col.size)
+    return ias.HostCsr(n, n, rp, col, val)
+
+
+def test_csr_wide_row_global_table():
+    A = wide_row()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, rep = ias.spgemm(A)
+    assert rep.max_row_nnz >= (1 << 19)
+    assert_csr_identical(got, ref, "wide row")
+    got_s, _ = ias.spgemm(A, order=ias.ORDER_SORTED)
+    rc, rv = sorted_form(ref)
+    np.testing.assert_array_equal(got_s.col, rc)
+    np.testing.assert_array_equal(bits(got_s.val), bits(rv))
+
+
+def test_csr_heavy_collisions_ordered_sums():
+    A = heavy_collisions()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, rep = ias.spgemm(A)
+    assert rep.max_row_products >= 30000
+    assert_csr_identical(got, ref, "heavy collisions")
+
+
 @pytest.mark.parametrize("case", cases_small()[:6], ids=lambda c: c[0])
 def test_csr_sorted_order(case):
     name, A, _ = case
