@@ -155,13 +155,16 @@ def main():
                  C.cast(C.c_void_p(c_ci.data_ptr()), ias.i32p),
                  C.cast(C.c_void_p(c_va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
     rep = ias.Report()
+    rep_s = ias.Report()
 
     def step():
         n = C.c_int64(0)
-        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None, None), "nnz")
+        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None,
+                                              C.byref(rep_s)), "nnz")
         Cm.nnz = cap
         ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
                                                   C.byref(rep)), "compute")
+        rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
         return rep
 
     for _ in range(args.warmup):

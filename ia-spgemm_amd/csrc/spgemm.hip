@@ -144,6 +144,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_rows(const int32_t *key, int6
 }
 
 // ---------------------------------------------------------------- symbolic kernels
+constexpr int LBITS_WORDS = 2048;   // first-touch bits staged in LDS (positions < 65536)
 template <int TEAM, int K, int LOG2S, int SEG, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, const int32_t *list,
                                                              int32_t count, int32_t *nnz_row) {
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, cons
     const int64_t row = idx < count ? list[idx] : -1;
     SymTable<false> tb{keys[team], nullptr, (uint32_t)LOG2S};
     const int32_t n = symbolic_row<TEAM, K, SEG, false>(A, B, row, tb, 0, 1, seg[team], scratch[team],
-                                                        nullptr, nullptr);
+                                                        nullptr, nullptr, nullptr);
     if (row >= 0 && Team<TEAM>::lane() == 0) nnz_row[row] = n;
 }
 
@@ -170,13 +171,20 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(Rows A, Rows B, const un
     __shared__ uint32_t minp[1 << LOG2S];
     __shared__ Seg<SEG, false> seg;
     __shared__ int scratch[64];
+    __shared__ uint32_t lbits[LBITS_WORDS];
     const unsigned long long it = items[blockIdx.x];
     const int64_t row = (int64_t)(it >> 32);
     const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
     const uint32_t np = nparts_of(prod[row], part_cap);
+    for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
     SymTable<true> tb{keys, minp, (uint32_t)LOG2S};
+    uint32_t *gbits = bm.bits + bm.off[row];
     const int32_t n = symbolic_row<TEAM, K, SEG, true>(A, B, row, tb, part, np, seg, scratch,
-                                                       bm.bits + bm.off[row], overflow);
+                                                       lbits, gbits, overflow);
+    // publish this partition's first-touch words (one atomic per non-zero word)
+    const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)prod[row] + 31) / 32);
+    for (int64_t w = threadIdx.x; w < W; w += TEAM)
+        if (lbits[w]) atomicOr(&gbits[w], lbits[w]);
     if (threadIdx.x == 0 && n > 0) atomicAdd(&nnz_row[row], n);
 }
 
@@ -633,9 +641,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if ((c = c1.count[3]) > 0)
         k_symbolic_lds<256, 4, 11, 256, 1><<<c, 256, 0, s>>>(A, B, lst(3), c, nnz);
     if ((c = c1.count[4]) > 0)
-        k_symbolic_lds<512, 4, 12, 256, 1><<<c, 512, 0, s>>>(A, B, lst(4), c, nnz);
+        k_symbolic_lds<256, 8, 12, 256, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, nnz);
     if ((c = c1.count[5]) > 0)
-        k_symbolic_lds<1024, 4, 13, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(5), c, nnz);
+        k_symbolic_lds<256, 8, 13, 256, 1><<<c, 256, 0, s>>>(A, B, lst(5), c, nnz);
     if ((c = c1.count[6]) > 0) {
         k_symbolic_part<512, 4, 13, 256><<<(unsigned)c1.items, 512, 0, s>>>(
             A, B, as<unsigned long long>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), PART_CAP, bm, nnz,
@@ -704,11 +712,11 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_r
     if ((c = num_count[2]) > 0)
         k_numeric_lds<32, 4, 7, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(A, B, lst(2), c, out);
     if ((c = num_count[3]) > 0)
-        k_numeric_lds<128, 4, 9, 128, 1><<<c, 128, 0, s>>>(A, B, lst(3), c, out);
+        k_numeric_lds<64, 4, 9, 64, 2><<<grid_for(c, 2), 128, 0, s>>>(A, B, lst(3), c, out);
     if ((c = num_count[4]) > 0)
-        k_numeric_lds<512, 4, 11, 256, 1><<<c, 512, 0, s>>>(A, B, lst(4), c, out);
+        k_numeric_lds<256, 4, 11, 256, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, out);
     if ((c = num_count[5]) > 0)
-        k_numeric_lds<1024, 2, 12, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(5), c, out);
+        k_numeric_lds<512, 4, 12, 256, 1><<<c, 512, 0, s>>>(A, B, lst(5), c, out);
     if ((c = num_count[6]) > 0)
         k_numeric_lds<1024, 2, 13, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(6), c, out);
     if (num_count[part_bin] > 0)

@@ -323,7 +323,8 @@ template <int TEAM, int K, int SEG, bool FT>
 __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, int64_t row,
                                                 const SymTable<FT> &table, uint32_t part,
                                                 uint32_t nparts, Seg<SEG, false> &sg,
-                                                int *scratch, uint32_t *bits, int *overflow) {
+                                                int *scratch, uint32_t *lbits, uint32_t *gbits,
+                                                int *overflow) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = 1u << table.log2s;
@@ -369,8 +370,10 @@ __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, in
         for (uint32_t s = lane; s < S; s += TEAM)
             if (table.key[s] != EMPTY_KEY) {
                 const uint32_t p = table.minp[s];
-                atomicOr(&bits[p >> 5], 1u << (p & 31));
+                if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+                else atomicOr(&gbits[p >> 5], 1u << (p & 31));
             }
+        TM::sync();
     }
     if (full) atomicOr(overflow, 1);
     return TM::sum(created, scratch);
@@ -518,8 +521,8 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
             if (cc != EMPTY_KEY) {
                 const uint32_t r = (uint32_t)(t.meta[s] >> MT::SHIFT);
                 const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
-                out.col[pos] = cc;
-                out.val[pos] = t.val[s];
+                __builtin_nontemporal_store(cc, &out.col[pos]);
+                __builtin_nontemporal_store(t.val[s], &out.val[pos]);
                 if (out.row_idx) out.row_idx[pos] = (int32_t)row;
             }
         }
@@ -549,8 +552,8 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
         }
         TM::sync();
         for (uint32_t e = lane; e < nnz; e += TEAM) {
-            out.col[o + e] = t.key[e];
-            out.val[o + e] = t.val[e];
+            __builtin_nontemporal_store(t.key[e], &out.col[o + e]);
+            __builtin_nontemporal_store(t.val[e], &out.val[o + e]);
             if (out.row_idx) out.row_idx[o + e] = (int32_t)row;
         }
     }
