@@ -32,6 +32,13 @@ namespace dev {
 constexpr int WAVE = 64;
 constexpr int32_t EMPTY_KEY = -1;
 
+// Timing-only ablation builds (tools/ablate.sh; never shipped): 1 = no
+// ordering rounds, 2 = no emission, 4 = no B value gather, 8 = no rank scan,
+// 16 = symbolic without hash inserts.
+#ifndef IAS_ABLATE
+#define IAS_ABLATE 0
+#endif
+
 // ---------------------------------------------------------------- row views
 // A "rows" operand: CSR (ptr != nullptr) or ELL (start = i*stride, len[i]).
 struct Rows {
@@ -357,7 +364,8 @@ __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, in
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 if (v[k] && (nparts <= 1 || part_of(c[k], nparts) == part)) {
-                    const int r = table.insert(c[k], pbase + p0 + k * TEAM + lane);
+                    const int r = (IAS_ABLATE & 16) ? (c[k] & 1)
+                                                    : table.insert(c[k], pbase + p0 + k * TEAM + lane);
                     created += r > 0 ? 1 : 0;
                     full |= r < 0;
                 }
@@ -435,7 +443,7 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
             }
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (pend[k]) prod[k] = sg.aval[jj[k]] * B.val[kk[k]];
+                if (pend[k]) prod[k] = (IAS_ABLATE & 4) ? sg.aval[jj[k]] : sg.aval[jj[k]] * B.val[kk[k]];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 slot[k] = 0;
@@ -451,16 +459,18 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
             }
             bool first_round = true;
             while (true) {
+#if !(IAS_ABLATE & 1)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (pend[k]) t.claim((uint32_t)slot[k], (uint32_t)(k * TEAM + lane));
                 TM::sync();
+#endif
                 bool win[K];
                 M rank[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const M m = pend[k] ? t.load((uint32_t)slot[k]) : (M)0;
-                    win[k] = pend[k] && ((m & MT::OWN) == (M)(k * TEAM + lane));
+                    win[k] = pend[k] && ((IAS_ABLATE & 1) || (m & MT::OWN) == (M)(k * TEAM + lane));
                     rank[k] = m >> MT::SHIFT;
                 }
                 if (first_round) {
@@ -468,8 +478,8 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
 #pragma unroll
                     for (int k = 0; k < K; ++k) ft[k] = win[k] && rank[k] == MT::RANK_NONE;
                     if constexpr (!PART) {
-                        int r[K];
-                        const int total = TM::template excl_count_items<K>(ft, r, scratch);
+                        int r[K] = {};
+                        const int total = (IAS_ABLATE & 8) ? 0 : TM::template excl_count_items<K>(ft, r, scratch);
 #pragma unroll
                         for (int k = 0; k < K; ++k)
                             if (ft[k]) rank[k] = (M)(base_rank + (uint32_t)r[k]);
@@ -512,7 +522,7 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
         TM::sync();
     }
     if (full) atomicOr(overflow, 1);
-    if (row < 0) return;
+    if (row < 0 || (IAS_ABLATE & 2)) return;
     const int64_t o = out.start(row);
     if constexpr (PART || WIDE) {
         const uint32_t nnz = PART ? (uint32_t)nnz_row : base_rank;
@@ -521,8 +531,9 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
             if (cc != EMPTY_KEY) {
                 const uint32_t r = (uint32_t)(t.meta[s] >> MT::SHIFT);
                 const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
-                __builtin_nontemporal_store(cc, &out.col[pos]);
-                __builtin_nontemporal_store(t.val[s], &out.val[pos]);
+                // scattered stores: plain (non-temporal partial lines measured 2x slower)
+                out.col[pos] = cc;
+                out.val[pos] = t.val[s];
                 if (out.row_idx) out.row_idx[pos] = (int32_t)row;
             }
         }
