@@ -144,20 +144,41 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_rows(const int32_t *key, int6
 }
 
 // ---------------------------------------------------------------- symbolic kernels
+// LDS tables are sized per bin at launch (dynamic LDS, any slot count), so a
+// row costs only the bytes its bin needs and more rows are resident per CU.
 constexpr int LBITS_WORDS = 2048;   // first-touch bits staged in LDS (positions < 65536)
-template <int TEAM, int K, int LOG2S, int SEG, int TPW>
+
+__host__ __device__ constexpr size_t round16(size_t b) { return (b + 15) & ~size_t(15); }
+
+template <int SEG, bool NUMERIC>
+__host__ __device__ constexpr size_t team_fixed_bytes() {
+    return round16(sizeof(Seg<SEG, NUMERIC>)) + 256;   // segment + 64-int scratch
+}
+// bytes of one team's region: [table | segment | scratch]
+template <int SEG>
+__host__ __device__ constexpr size_t sym_team_bytes(uint32_t S) {
+    return round16(4ull * S) + team_fixed_bytes<SEG, false>();
+}
+template <int SEG>
+__host__ __device__ constexpr size_t num_team_bytes(uint32_t S) {
+    return round16(8ull * S) + 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
+}
+
+template <int TEAM, int K, int SEG, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, const int32_t *list,
-                                                             int32_t count, int32_t *nnz_row) {
+                                                             int32_t count, uint32_t S, int32_t *nnz_row) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
-    __shared__ int32_t keys[TPW][1 << LOG2S];
-    __shared__ Seg<SEG, false> seg[TPW];
-    __shared__ int scratch[TPW][64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    unsigned char *base = smem + (size_t)team * sym_team_bytes<SEG>(S);
+    int32_t *keys = (int32_t *)base;
+    auto &seg = *(Seg<SEG, false> *)(base + round16(4ull * S));
+    int *scratch = (int *)(base + round16(4ull * S) + round16(sizeof(Seg<SEG, false>)));
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
     const int64_t row = idx < count ? list[idx] : -1;
-    SymTable<false> tb{keys[team], nullptr, (uint32_t)LOG2S};
-    const int32_t n = symbolic_row<TEAM, K, SEG, false>(A, B, row, tb, 0, 1, seg[team], scratch[team],
-                                                        nullptr, nullptr, nullptr);
+    SymTable<false> tb{keys, nullptr, S};
+    const int32_t n = symbolic_row<TEAM, K, SEG, false>(A, B, row, tb, 0, 1, seg, scratch, nullptr,
+                                                        nullptr, nullptr);
     if (row >= 0 && Team<TEAM>::lane() == 0) nnz_row[row] = n;
 }
 
@@ -177,7 +198,7 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(Rows A, Rows B, const un
     const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
     const uint32_t np = nparts_of(prod[row], part_cap);
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
-    SymTable<true> tb{keys, minp, (uint32_t)LOG2S};
+    SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
     const int32_t n = symbolic_row<TEAM, K, SEG, true>(A, B, row, tb, part, np, seg, scratch,
                                                        lbits, gbits, overflow);
@@ -208,23 +229,24 @@ __global__ __launch_bounds__(256) void k_bitmap_prefix(const int32_t *list, int3
 }
 
 // ---------------------------------------------------------------- numeric kernels
-template <int TEAM, int K, int LOG2S, int SEG, int TPW>
+template <int TEAM, int K, int SEG, int TPW, int PER>
 __global__ __launch_bounds__(TEAM *TPW) void k_numeric_lds(Rows A, Rows B, const int32_t *list,
-                                                            int32_t count, Out out) {
+                                                            int32_t count, uint32_t S, Out out) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
-    constexpr int PER = (1 << LOG2S) / TEAM;
-    static_assert(PER >= 1 && PER <= 8, "emission keeps S/TEAM slots per lane in registers");
-    __shared__ int32_t keys[TPW][1 << LOG2S];
-    __shared__ uint32_t meta[TPW][1 << LOG2S];
-    __shared__ double vals[TPW][1 << LOG2S];
-    __shared__ Seg<SEG, true> seg[TPW];
-    __shared__ int scratch[TPW][64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    unsigned char *base = smem + (size_t)team * num_team_bytes<SEG>(S);
+    double *vals = (double *)base;
+    int32_t *keys = (int32_t *)(base + round16(8ull * S));
+    uint32_t *meta = (uint32_t *)(base + round16(8ull * S) + round16(4ull * S));
+    unsigned char *fixed = base + round16(8ull * S) + 2 * round16(4ull * S);
+    auto &seg = *(Seg<SEG, true> *)fixed;
+    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, true>)));
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
     const int64_t row = idx < count ? list[idx] : -1;
-    NumTable<false> tb{keys[team], meta[team], vals[team], (uint32_t)LOG2S};
-    numeric_row<TEAM, K, SEG, false, false, PER>(A, B, row, tb, 0, 1, nullptr, nullptr, seg[team],
-                                                  scratch[team], out, 0, nullptr);
+    NumTable<false> tb{keys, meta, vals, S};
+    numeric_row<TEAM, K, SEG, false, false, PER>(A, B, row, tb, 0, 1, nullptr, nullptr, seg, scratch,
+                                                  out, 0, nullptr);
 }
 
 template <int TEAM, int K, int LOG2S, int SEG>
@@ -241,7 +263,7 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(Rows A, Rows B, const uns
     const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
     const int32_t nnz = nnz_row[row];
     const uint32_t np = nparts_of(nnz, part_cap);
-    NumTable<false> tb{keys, meta, vals, (uint32_t)LOG2S};
+    NumTable<false> tb{keys, meta, vals, 1u << LOG2S};
     numeric_row<TEAM, K, SEG, false, true, 1>(A, B, row, tb, part, np, bm.bits + bm.off[row],
                                               bm.pref + bm.off[row], seg, scratch, out, nnz, overflow);
 }
@@ -264,7 +286,7 @@ __global__ __launch_bounds__(TEAM) void k_numeric_global(Rows A, Rows B, const i
     const uint64_t S = 1ull << l2;
     char *base = ws + (uint64_t)ws_off[idx] * 20ull;
     NumTable<true> tb{(int32_t *)base, (unsigned long long *)(base + S * 4ull),
-                      (double *)(base + S * 12ull), l2};
+                      (double *)(base + S * 12ull), (uint32_t)S};
     numeric_row<TEAM, K, SEG, true, false, 1>(A, B, row, tb, 0, 1, nullptr, nullptr, seg, scratch,
                                               out, 0, nullptr);
 }
@@ -491,15 +513,43 @@ using namespace ias::dev;
 // first-touch bitmap.  Numeric bins by nnz with 16-byte slots; rows beyond
 // 5460 nnz are hash-partitioned (4096 per partition); rows at >= 2^19 - 1 nnz
 // (beyond the 19-bit rank field) use a per-row table in global memory.
+static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
 constexpr int32_t LDS_MAX = 5460;
 constexpr int32_t PART_CAP = 4096;
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
 
+// LDS bins: upper bound of the key (products for symbolic, nnz for numeric),
+// kernel configuration, and table slots S = ceil(1.5 * upper).
+struct BinCfg {
+    int32_t upper;
+    int32_t cfg;
+};
+static constexpr BinCfg SYM_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {1024, 4}, {1536, 5},
+                                   {2048, 5}, {2730, 5}, {3640, 6}, {4550, 6}, {LDS_MAX, 6}};
+static constexpr BinCfg NUM_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
+                                   {512, 4},  {768, 5},  {1024, 5}, {1365, 5}, {1820, 6},
+                                   {2430, 6}, {3240, 7}, {4320, 7}, {LDS_MAX, 7}};
+constexpr int N_SYM_BINS = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
+constexpr int N_NUM_BINS = sizeof(NUM_BINS) / sizeof(NUM_BINS[0]);
+static_assert(N_NUM_BINS + 3 <= MAX_BINS, "bins");
+
+static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
+
+// TEAM * PER of each numeric configuration in num_bin(): the emission loop
+// visits that many slots, so it must cover every bin's S.
+static constexpr uint32_t NUM_CFG_EMIT[] = {48, 96, 192, 384, 768, 2048, 4096, 8192};
+static constexpr bool num_bins_covered() {
+    for (int i = 0; i < N_NUM_BINS; ++i)
+        if (NUM_CFG_EMIT[NUM_BINS[i].cfg] < slots_for(NUM_BINS[i].upper)) return false;
+    return true;
+}
+static_assert(num_bins_covered(), "numeric emission does not cover a bin's table");
+
 static BinSpec sym_spec() {
     BinSpec s{};
-    s.nlds = 5;
-    const int32_t u[] = {0, 64, 256, 1024, 2730, LDS_MAX};
-    for (int i = 0; i <= 5; ++i) s.upper[i] = u[i];
+    s.nlds = N_SYM_BINS;
+    for (int i = 0; i < N_SYM_BINS; ++i) s.upper[i + 1] = SYM_BINS[i].upper;
     s.part_cap = PART_CAP;
     s.wide_min = 0;
     s.ft = 1;
@@ -509,9 +559,8 @@ static BinSpec sym_spec() {
 
 static BinSpec num_spec() {
     BinSpec s{};
-    s.nlds = 6;
-    const int32_t u[] = {0, 16, 64, 256, 1024, 2730, LDS_MAX};
-    for (int i = 0; i <= 6; ++i) s.upper[i] = u[i];
+    s.nlds = N_NUM_BINS;
+    for (int i = 0; i < N_NUM_BINS; ++i) s.upper[i + 1] = NUM_BINS[i].upper;
     s.part_cap = PART_CAP;
     s.wide_min = WIDE_MIN;
     s.ft = 0;
@@ -519,7 +568,61 @@ static BinSpec num_spec() {
     return s;
 }
 
-static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+// Allow up to the full 160 KiB of LDS for a dynamically sized kernel (once).
+template <typename F>
+static void allow_lds(F kernel) {
+    static bool done = false;
+    if (!done) {
+        hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        done = true;
+    }
+}
+
+template <int TEAM, int K, int SEG, int TPW>
+static void sym_launch(int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B, const int32_t *list,
+                       int32_t *nnz) {
+    auto kern = k_symbolic_lds<TEAM, K, SEG, TPW>;
+    allow_lds(kern);
+    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(S);
+    kern<<<grid_for(c, TPW), TEAM * TPW, lds, s>>>(A, B, list, c, S, nnz);
+}
+
+static void sym_bin(int cfg, int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B,
+                    const int32_t *list, int32_t *nnz) {
+    switch (cfg) {
+        case 0: sym_launch<16, 4, 16, 16>(c, S, s, A, B, list, nnz); break;
+        case 1: sym_launch<32, 4, 32, 8>(c, S, s, A, B, list, nnz); break;
+        case 2: sym_launch<64, 4, 64, 4>(c, S, s, A, B, list, nnz); break;
+        case 3: sym_launch<64, 8, 64, 4>(c, S, s, A, B, list, nnz); break;
+        case 4: sym_launch<128, 8, 128, 1>(c, S, s, A, B, list, nnz); break;
+        case 5: sym_launch<256, 8, 256, 1>(c, S, s, A, B, list, nnz); break;
+        default: sym_launch<512, 8, 256, 1>(c, S, s, A, B, list, nnz); break;
+    }
+}
+
+template <int TEAM, int K, int SEG, int TPW, int PER>
+static void num_launch(int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B, const int32_t *list,
+                       const Out &out) {
+    auto kern = k_numeric_lds<TEAM, K, SEG, TPW, PER>;
+    allow_lds(kern);
+    const size_t lds = (size_t)TPW * num_team_bytes<SEG>(S);
+    kern<<<grid_for(c, TPW), TEAM * TPW, lds, s>>>(A, B, list, c, S, out);
+}
+
+static void num_bin(int cfg, int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B,
+                    const int32_t *list, const Out &out) {
+    switch (cfg) {
+        case 0: num_launch<16, 4, 16, 16, 3>(c, S, s, A, B, list, out); break;
+        case 1: num_launch<32, 4, 32, 8, 3>(c, S, s, A, B, list, out); break;
+        case 2: num_launch<64, 4, 64, 4, 3>(c, S, s, A, B, list, out); break;
+        case 3: num_launch<64, 4, 64, 2, 6>(c, S, s, A, B, list, out); break;
+        case 4: num_launch<128, 4, 128, 1, 6>(c, S, s, A, B, list, out); break;
+        case 5: num_launch<256, 4, 256, 1, 8>(c, S, s, A, B, list, out); break;
+        case 6: num_launch<512, 4, 256, 1, 8>(c, S, s, A, B, list, out); break;
+        default: num_launch<1024, 2, 256, 1, 8>(c, S, s, A, B, list, out); break;
+    }
+}
+
 
 #define HIPC(x)                                                                   \
     do {                                                                          \
@@ -634,21 +737,14 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
     }
     int c;
-    if ((c = c1.count[1]) > 0)
-        k_symbolic_lds<16, 4, 7, 16, 16><<<grid_for(c, 16), 256, 0, s>>>(A, B, lst(1), c, nnz);
-    if ((c = c1.count[2]) > 0)
-        k_symbolic_lds<64, 4, 9, 64, 4><<<grid_for(c, 4), 256, 0, s>>>(A, B, lst(2), c, nnz);
-    if ((c = c1.count[3]) > 0)
-        k_symbolic_lds<256, 4, 11, 256, 1><<<c, 256, 0, s>>>(A, B, lst(3), c, nnz);
-    if ((c = c1.count[4]) > 0)
-        k_symbolic_lds<256, 8, 12, 256, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, nnz);
-    if ((c = c1.count[5]) > 0)
-        k_symbolic_lds<256, 8, 13, 256, 1><<<c, 256, 0, s>>>(A, B, lst(5), c, nnz);
-    if ((c = c1.count[6]) > 0) {
+    for (int b = 1; b <= ss.nlds; ++b)
+        if ((c = c1.count[b]) > 0)
+            sym_bin(SYM_BINS[b - 1].cfg, c, slots_for(SYM_BINS[b - 1].upper), s, A, B, lst(b), nnz);
+    if ((c = c1.count[ss.nlds + 1]) > 0) {
         k_symbolic_part<512, 4, 13, 256><<<(unsigned)c1.items, 512, 0, s>>>(
             A, B, as<unsigned long long>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), PART_CAP, bm, nnz,
             &dc2->overflow);
-        k_bitmap_prefix<<<c, 256, 0, s>>>(lst(6), c, as<int32_t>(bufs[B_PROD]), bm);
+        k_bitmap_prefix<<<c, 256, 0, s>>>(lst(ss.nlds + 1), c, as<int32_t>(bufs[B_PROD]), bm);
     }
     HIPC(hipGetLastError());
 
@@ -707,18 +803,9 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_r
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     HIPC(hipEventRecord(ev[3], s));
     int c;
-    if ((c = num_count[1]) > 0)
-        k_numeric_lds<16, 4, 5, 16, 16><<<grid_for(c, 16), 256, 0, s>>>(A, B, lst(1), c, out);
-    if ((c = num_count[2]) > 0)
-        k_numeric_lds<32, 4, 7, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(A, B, lst(2), c, out);
-    if ((c = num_count[3]) > 0)
-        k_numeric_lds<64, 4, 9, 64, 2><<<grid_for(c, 2), 128, 0, s>>>(A, B, lst(3), c, out);
-    if ((c = num_count[4]) > 0)
-        k_numeric_lds<256, 4, 11, 256, 1><<<c, 256, 0, s>>>(A, B, lst(4), c, out);
-    if ((c = num_count[5]) > 0)
-        k_numeric_lds<512, 4, 12, 256, 1><<<c, 512, 0, s>>>(A, B, lst(5), c, out);
-    if ((c = num_count[6]) > 0)
-        k_numeric_lds<1024, 2, 13, 256, 1><<<c, 1024, 0, s>>>(A, B, lst(6), c, out);
+    for (int b = 1; b <= ns.nlds; ++b)
+        if ((c = num_count[b]) > 0)
+            num_bin(NUM_BINS[b - 1].cfg, c, slots_for(NUM_BINS[b - 1].upper), s, A, B, lst(b), out);
     if (num_count[part_bin] > 0)
         k_numeric_part<1024, 2, 13, 256><<<(unsigned)num_items, 1024, 0, s>>>(
             A, B, as<unsigned long long>(bufs[B_NITEM]), as<int32_t>(bufs[B_NNZ]), PART_CAP, bm, out,

@@ -8,7 +8,7 @@
 
 namespace ias {
 
-constexpr int MAX_BINS = 10;   // 0 = empty rows, 1..nlds = LDS bins, nlds+1 = hash
+constexpr int MAX_BINS = 18;   // 0 = empty rows, 1..nlds = LDS bins, nlds+1 = hash
                                // partitions, nlds+2 = global-memory table
 
 // How a pass bins its rows by `key` (products or nnz).

@@ -189,9 +189,10 @@ struct Team {
     }
 };
 
-// table slot hash and (independent) partition hash
-__device__ __forceinline__ uint32_t slot_hash(int32_t c, uint32_t log2s) {
-    return log2s ? (((uint32_t)c * 0x9E3779B1u) >> (32u - log2s)) : 0u;
+// table slot hash (multiply-shift onto [0, size), any size) and an
+// independent partition hash
+__device__ __forceinline__ uint32_t slot_hash(int32_t c, uint32_t size) {
+    return (uint32_t)(((uint64_t)((uint32_t)c * 0x9E3779B1u) * size) >> 32);
 }
 __device__ __forceinline__ uint32_t part_of(int32_t c, uint32_t nparts) {
     const uint32_t h = ((uint32_t)c * 0x85EBCA6Bu) ^ ((uint32_t)c >> 16);
@@ -206,17 +207,16 @@ template <bool FT>
 struct SymTable {
     int32_t *key;
     uint32_t *minp;   // FT only
-    uint32_t log2s;
+    uint32_t size;
     __device__ __forceinline__ int insert(int32_t c, uint32_t p) const {
-        const uint32_t m = (1u << log2s) - 1u;
-        uint32_t s = slot_hash(c, log2s);
-        for (uint32_t probe = 0; probe <= m; ++probe) {
+        uint32_t s = slot_hash(c, size);
+        for (uint32_t probe = 0; probe < size; ++probe) {
             const int32_t prev = atomicCAS(&key[s], EMPTY_KEY, c);
             if (prev == EMPTY_KEY || prev == c) {
                 if constexpr (FT) atomicMin(&minp[s], p);
                 return prev == EMPTY_KEY ? 1 : 0;
             }
-            s = (s + 1u) & m;
+            s = (s + 1u == size) ? 0u : s + 1u;
         }
         return -1;
     }
@@ -251,15 +251,14 @@ struct NumTable {
     int32_t *key;
     M *meta;
     double *val;
-    uint32_t log2s;
+    uint32_t size;
 
     __device__ __forceinline__ int find_or_insert(int32_t c) const {
-        const uint32_t m = (1u << log2s) - 1u;
-        uint32_t s = slot_hash(c, log2s);
-        for (uint32_t probe = 0; probe <= m; ++probe) {
+        uint32_t s = slot_hash(c, size);
+        for (uint32_t probe = 0; probe < size; ++probe) {
             const int32_t prev = atomicCAS(&key[s], EMPTY_KEY, c);
             if (prev == EMPTY_KEY || prev == c) return (int)s;
-            s = (s + 1u) & m;
+            s = (s + 1u == size) ? 0u : s + 1u;
         }
         return -1;
     }
@@ -334,7 +333,7 @@ __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, in
                                                 int *overflow) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
-    const uint32_t S = 1u << table.log2s;
+    const uint32_t S = table.size;
     for (uint32_t s = lane; s < S; s += TEAM) {
         table.key[s] = EMPTY_KEY;
         if constexpr (FT) table.minp[s] = 0xFFFFFFFFu;
@@ -405,7 +404,7 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
     static_assert((unsigned long long)TEAM * K < (unsigned long long)MT::OWN,
                   "item ids must fit the owner field");
     const int lane = TM::lane();
-    const uint32_t S = 1u << t.log2s;
+    const uint32_t S = t.size;
     for (uint32_t s = lane; s < S; s += TEAM) {
         t.key[s] = EMPTY_KEY;
         t.meta[s] = MT::INIT;
@@ -540,7 +539,7 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
     } else {
         // LDS-staged emission: slots -> registers -> (col, val) at their final
         // position in the key/val arrays -> coalesced stores of the row.
-        // PER = S / TEAM slots per lane (compile-time, from the kernel).
+        // PER >= ceil(S / TEAM) slots per lane (compile-time, from the kernel).
         const uint32_t nnz = base_rank;
         int32_t kc[PER];
         uint32_t kr[PER];
@@ -548,9 +547,12 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const uint32_t s = (uint32_t)i * TEAM + lane;
-            kc[i] = t.key[s];
-            kr[i] = (uint32_t)(t.meta[s] >> MT::SHIFT);
-            kv[i] = t.val[s];
+            kc[i] = EMPTY_KEY;
+            if (s < S) {
+                kc[i] = t.key[s];
+                kr[i] = (uint32_t)(t.meta[s] >> MT::SHIFT);
+                kv[i] = t.val[s];
+            }
         }
         TM::sync();
 #pragma unroll
