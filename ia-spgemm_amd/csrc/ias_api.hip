@@ -437,14 +437,14 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     }
     dev::Rows ra{dA->row_ptr, nullptr, 0, dA->col, dA->val};
     dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
     const int64_t nnz = plan->nnz_total;
 
     ias_csr D{};
     IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
     HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
                         hipMemcpyDeviceToDevice, s));
-    dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0};
+    dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0, nullptr};
     ias_status stn = plan->numeric(ra, rb, out, rep);
     if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
         stn = ias_sort_rows_device(plan, D.row_ptr, A->rows, D.col, D.val, plan->max_nnz);
@@ -495,7 +495,7 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
     }
     dev::Rows ra{ap, nullptr, 0, ac, av};
     dev::Rows rb{bp, nullptr, 0, bc, bv};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
     const int64_t nnz = plan->nnz_total;
     ias_coo D{};
     D.rows = A->rows; D.cols = B->cols; D.nnz = nnz; D.memory = IAS_MEMORY_DEVICE;
@@ -514,7 +514,7 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
     D.row = (int32_t *)p1; D.col = (int32_t *)p2; D.val = (double *)p3;
     HIPC(hipMemcpyAsync(D.row_offset, plan->bufs[ias_plan::B_PTR].p,
                         sizeof(int64_t) * (A->rows + 1), hipMemcpyDeviceToDevice, s));
-    dev::Out out{D.row_offset, 0, D.col, D.val, D.row, o.order == IAS_ORDER_SORTED ? 0 : 1, 1};
+    dev::Out out{D.row_offset, 0, D.col, D.val, D.row, o.order == IAS_ORDER_SORTED ? 0 : 1, 1, nullptr};
     ias_status stn = plan->numeric(ra, rb, out, rep);
     if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
         stn = ias_sort_rows_device(plan, D.row_offset, A->rows, D.col, D.val, plan->max_nnz);
@@ -565,7 +565,7 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
     }
     dev::Rows ra{nullptr, an, A->max_nnz_per_row, ac, av};
     dev::Rows rb{nullptr, bn, B->max_nnz_per_row, bc, bv};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, (int64_t)ak, rep));
     const int32_t K = plan->max_nnz;
     ias_ell D{};
     D.rows = A->rows; D.cols = B->cols; D.nnz = plan->nnz_total; D.max_nnz_per_row = K;
@@ -585,7 +585,7 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
                         hipMemcpyDeviceToDevice, s));
     HIPC(hipMemsetAsync(D.col, 0, sizeof(int32_t) * ck, s));
     HIPC(hipMemsetAsync(D.val, 0, sizeof(double) * ck, s));
-    dev::Out out{nullptr, K, D.col, D.val, nullptr, 0, 0};
+    dev::Out out{nullptr, K, D.col, D.val, nullptr, 0, 0, nullptr};
     ias_status stn = plan->numeric(ra, rb, out, rep);
     if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
         stn = ias_sort_rows_ell_device(plan, D.nnz_row, A->rows, K, D.col, D.val);
@@ -623,7 +623,7 @@ extern "C" ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, cons
     if (rep) memset(rep, 0, sizeof *rep);
     dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
     dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, rep));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
     plan->last_a = A->col;
     plan->last_b = B->col;
     *nnz_c = plan->nnz_total;
@@ -655,7 +655,7 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
     C->nnz = plan->nnz_total;
     dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
     dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
-    dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0};
+    dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0, nullptr};
     IAS_TRY(plan->numeric(ra, rb, out, rep));
     if (order == IAS_ORDER_SORTED)
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, plan->max_nnz));

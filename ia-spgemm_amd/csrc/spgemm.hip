@@ -12,22 +12,69 @@
 namespace ias {
 namespace dev {
 
+// ---------------------------------------------------------------- binning
+// Bin of a row with key k (products for symbolic, nnz for numeric/sort) and
+// products `prod` (numeric class test).  Bin numbering: 0 = nothing to do,
+// 1..nval = value LDS bins, nval+1 = hash partitions, nval+2 = global table,
+// nval+3.. = direct-write LDS bins.
+__device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
+    return (uint32_t)((key + cap - 1) / cap);
+}
+
+__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod) {
+    if (k <= 0) return 0;
+    if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
+    const bool val_class =
+        sp.ratio_den == 0 || (int64_t)prod * sp.ratio_den > (int64_t)k * sp.ratio_num;
+    if (val_class)
+        for (int i = 1; i <= sp.nval; ++i)
+            if (k <= sp.upper[i]) return i;
+    for (int i = 0; i < sp.ndw; ++i)
+        if (k <= sp.upper[sp.nval + 3 + i]) return sp.nval + 3 + i;
+    return sp.nval + 1;
+}
+
+// Block-level count of rows per bin (+ partition items, bitmap words and
+// global-table slots of the rows that need them) into the Counters totals.
+template <int BLOCK>
+__device__ __forceinline__ void count_bins(const BinSpec &sp, int b, int32_t k, Counters *cnt) {
+    __shared__ int hist[MAX_BINS];
+    for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK) hist[i] = 0;
+    __syncthreads();
+    if (b > 0) {
+        atomicAdd(&hist[b], 1);
+        if (b == sp.nval + 1) {
+            atomicAdd(&cnt->items, (unsigned long long)nparts_of(k, sp.part_cap));
+            if (sp.ft) atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
+        } else if (b == sp.nval + 2) {
+            const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
+            unsigned long long S = 1;
+            while (S < need) S <<= 1;
+            atomicAdd(&cnt->ws_slots, S);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK)
+        if (i > 0 && hist[i] > 0) atomicAdd(&cnt->count[i], hist[i]);
+}
+
 // ---------------------------------------------------------------- analysis
-// Products per row (GetFlop per row).  A block owns 256 consecutive rows and
-// spreads their A entries over its threads (a hub row does not serialise on
-// one lane).  Also accumulates total flops and the max products per row.
+// Products per row (GetFlop per row) and the expanded A (AxView).  A block
+// owns 256 consecutive rows and spreads their A entries over its threads (a
+// hub row does not serialise on one lane).  Also accumulates total flops, the
+// max products per row, and the symbolic bin counts.
 constexpr int AN_BLOCK = 256;
 
-__global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64_t rows,
-                                                           int32_t *prod,
-                                                           unsigned long long *flops,
-                                                           int32_t *max_prod) {
+__global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64_t rows, AxOut ax,
+                                                           int64_t a_entries, int32_t *prod,
+                                                           BinSpec spec, Counters *cnt) {
     __shared__ int64_t start[AN_BLOCK];
     __shared__ int32_t pref[AN_BLOCK + 1];
     __shared__ unsigned long long acc[AN_BLOCK];
     __shared__ int scratch[8];
     const int t = threadIdx.x;
     const int64_t r = (int64_t)blockIdx.x * AN_BLOCK + t;
+    const int64_t abase = A.base();
     int64_t s = 0;
     int32_t n = 0;
     if (r < rows) A.row(r, s, n);
@@ -43,16 +90,26 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
     const int32_t E = pref[AN_BLOCK];
     for (int32_t e = t; e < E; e += AN_BLOCK) {
         const int lo = seg_find(pref, AN_BLOCK, e);
-        const int32_t j = A.col[start[lo] + (e - pref[lo])];
+        const int64_t ea = start[lo] + (e - pref[lo]);
+        const int32_t j = A.col[ea];
         int64_t bs;
         int32_t bn;
         B.row(j, bs, bn);
+        const int64_t q = ea - abase;
+        if (q >= 0 && q < a_entries) {
+            ax.bstart[q] = bs;
+            ax.blen[q] = bn;
+            ax.aval[q] = A.val[ea];
+        } else {
+            cnt->overflow = 1;   // row pointer disagrees with the declared entry count
+        }
         atomicAdd(&acc[lo], (unsigned long long)bn);
     }
     __syncthreads();
     const unsigned long long mine = acc[t];
     const int mx0 = (int)min(mine, (unsigned long long)INT32_MAX);
     if (r < rows) prod[r] = mx0;
+    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0) : -1, mx0, cnt);
     __shared__ unsigned long long red_sum[AN_BLOCK / WAVE];
     __shared__ int red_max[AN_BLOCK / WAVE];
     unsigned long long sm = (r < rows) ? mine : 0ull;
@@ -73,72 +130,83 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
             S += red_sum[i];
             MX = max(MX, red_max[i]);
         }
-        atomicAdd(flops, S);
-        atomicMax(max_prod, MX);
+        atomicAdd(&cnt->flops, S);
+        atomicMax(&cnt->max_prod, MX);
     }
 }
 
-// ---------------------------------------------------------------- binning
 constexpr int BIN_BLOCK = 256;
 
-__device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
-    return (uint32_t)((key + cap - 1) / cap);
+// Counting pass of a binning (numeric and sort binnings; the symbolic one is
+// fused into k_row_products).  prod may be null (class test off).
+__global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, const int32_t *prod,
+                                                         int64_t rows, BinSpec spec, Counters *cnt) {
+    const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + threadIdx.x;
+    int b = -1;
+    int32_t k = 0;
+    if (r < rows) {
+        k = key[r];
+        b = bin_of(spec, k, prod ? prod[r] : k);
+    }
+    count_bins<BIN_BLOCK>(spec, b, k, cnt);
 }
 
-// key[i] -> bin (BinSpec).  LDS and wide bins get row lists; the partition
-// bin gets its rows listed AND one (row << 32 | part) work item per
-// partition; FT rows get a first-touch bitmap offset; wide rows a
-// global-table offset of nextpow2(ceil(key*3/2)) slots.
-__global__ __launch_bounds__(BIN_BLOCK) void k_bin_rows(const int32_t *key, int64_t rows,
-                                                        BinSpec spec, int32_t *lists,
-                                                        unsigned long long *items,
-                                                        int64_t *bm_off, int64_t *ws_off,
-                                                        int32_t *nnz_row, Counters *cnt) {
+// Scatter pass: every listed row gets a RowRef in its bin's compact list
+// (bins laid out in bin order, offsets = prefix of the counted totals);
+// partitioned rows get one PartItem per partition (+ a bitmap offset when
+// FT); global-table rows a workspace offset of nextpow2(ceil(k*3/2)) slots.
+__global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, const int32_t *prod,
+                                                           int64_t rows, BinSpec spec, Rows A,
+                                                           RowRef *lists, PartItem *items,
+                                                           int64_t *bm_off, int64_t *ws_off,
+                                                           int32_t *nnz_row, Counters *cnt) {
     __shared__ int hist[MAX_BINS];
-    __shared__ int base[MAX_BINS];
+    __shared__ int64_t base[MAX_BINS];
+    __shared__ int64_t bin_start[MAX_BINS];
     const int t = threadIdx.x;
     if (t < MAX_BINS) hist[t] = 0;
+    if (t == 0) {
+        int64_t acc = 0;
+        for (int i = 0; i < MAX_BINS; ++i) {
+            bin_start[i] = acc;
+            acc += i > 0 ? cnt->count[i] : 0;
+        }
+    }
     __syncthreads();
     const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + t;
-    const int part_bin = spec.nlds + 1, wide_bin = spec.nlds + 2;
+    const int part_bin = spec.nval + 1, wide_bin = spec.nval + 2;
     int b = -1, local = 0;
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
-        if (k <= 0) {
-            b = 0;
-            if (spec.zero_nnz) nnz_row[r] = 0;
-        } else {
-            if (spec.wide_min > 0 && k >= spec.wide_min) {
-                b = wide_bin;
-            } else {
-                b = part_bin;
-                for (int i = 1; i <= spec.nlds; ++i)
-                    if (k <= spec.upper[i]) {
-                        b = i;
-                        break;
-                    }
-            }
-            local = atomicAdd(&hist[b], 1);
-        }
+        b = bin_of(spec, k, prod ? prod[r] : k);
+        if (b == 0 && spec.zero_nnz) nnz_row[r] = 0;
+        if (b > 0) local = atomicAdd(&hist[b], 1);
     }
     __syncthreads();
-    if (t > 0 && t < MAX_BINS && hist[t] > 0) base[t] = atomicAdd(&cnt->count[t], hist[t]);
+    if (t > 0 && t < MAX_BINS && hist[t] > 0) base[t] = atomicAdd(&cnt->cursor[t], hist[t]);
     __syncthreads();
     if (b > 0) {
-        const int pos = base[b] + local;
-        lists[(int64_t)b * rows + pos] = (int32_t)r;
+        const int64_t within = base[b] + local;
+        RowRef ref;
+        int64_t s;
+        int32_t n;
+        A.row(r, s, n);
+        ref.q0 = s - A.base();
+        ref.row = (int32_t)r;
+        ref.n = n;
+        lists[bin_start[b] + within] = ref;
         if (b == part_bin) {
             const uint32_t np = nparts_of(k, spec.part_cap);
-            const unsigned long long at = atomicAdd(&cnt->items, (unsigned long long)np);
-            for (uint32_t q = 0; q < np; ++q) items[at + q] = ((unsigned long long)r << 32) | q;
-            if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
+            const unsigned long long at = atomicAdd(&cnt->items_cur, (unsigned long long)np);
+            for (uint32_t q = 0; q < np; ++q) items[at + q] = PartItem{ref, q, np};
+            if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
             if (spec.zero_nnz) nnz_row[r] = 0;
         } else if (b == wide_bin) {
             const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
             unsigned long long S = 1;
             while (S < need) S <<= 1;
-            ws_off[pos] = (int64_t)atomicAdd(&cnt->ws_slots, S);
+            ws_off[within] = (int64_t)atomicAdd(&cnt->ws_cur, S);
         }
     }
 }
@@ -160,12 +228,21 @@ __host__ __device__ constexpr size_t sym_team_bytes(uint32_t S) {
     return round16(4ull * S) + team_fixed_bytes<SEG, false>();
 }
 template <int SEG>
-__host__ __device__ constexpr size_t num_team_bytes(uint32_t S) {
+__host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
     return round16(8ull * S) + 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
+}
+template <int SEG>
+__host__ __device__ constexpr size_t dw_team_bytes(uint32_t S) {
+    return 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
+}
+
+__device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_t count) {
+    if (idx < count) return list[idx];
+    return RowRef{0, -1, 0};
 }
 
 template <int TEAM, int K, int SEG, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, const int32_t *list,
+__global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(AxView ax, Rows B, const RowRef *list,
                                                              int32_t count, uint32_t S, int32_t *nnz_row) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -174,34 +251,31 @@ __global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(Rows A, Rows B, cons
     int32_t *keys = (int32_t *)base;
     auto &seg = *(Seg<SEG, false> *)(base + round16(4ull * S));
     int *scratch = (int *)(base + round16(4ull * S) + round16(sizeof(Seg<SEG, false>)));
-    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx] : -1;
+    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
     SymTable<false> tb{keys, nullptr, S};
-    const int32_t n = symbolic_row<TEAM, K, SEG, false>(A, B, row, tb, 0, 1, seg, scratch, nullptr,
+    const int32_t n = symbolic_row<TEAM, K, SEG, false>(ax, B, ref, tb, 0, 1, seg, scratch, nullptr,
                                                         nullptr, nullptr);
-    if (row >= 0 && Team<TEAM>::lane() == 0) nnz_row[row] = n;
+    if (ref.row >= 0 && Team<TEAM>::lane() == 0) nnz_row[ref.row] = n;
 }
 
 // One workgroup per (row, hash partition): distinct columns of the partition
 // (added to nnz_row) and the first-touch bits of the row's bitmap.
 template <int TEAM, int K, int LOG2S, int SEG>
-__global__ __launch_bounds__(TEAM) void k_symbolic_part(Rows A, Rows B, const unsigned long long *items,
-                                                        const int32_t *prod, int32_t part_cap,
-                                                        Bitmap bm, int32_t *nnz_row, int *overflow) {
+__global__ __launch_bounds__(TEAM) void k_symbolic_part(AxView ax, Rows B, const PartItem *items,
+                                                        const int32_t *prod, Bitmap bm,
+                                                        int32_t *nnz_row, int *overflow) {
     __shared__ int32_t keys[1 << LOG2S];
     __shared__ uint32_t minp[1 << LOG2S];
     __shared__ Seg<SEG, false> seg;
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
-    const unsigned long long it = items[blockIdx.x];
-    const int64_t row = (int64_t)(it >> 32);
-    const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
-    const uint32_t np = nparts_of(prod[row], part_cap);
+    const PartItem it = items[blockIdx.x];
+    const int64_t row = it.ref.row;
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
     SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
-    const int32_t n = symbolic_row<TEAM, K, SEG, true>(A, B, row, tb, part, np, seg, scratch,
-                                                       lbits, gbits, overflow);
+    const int32_t n = symbolic_row<TEAM, K, SEG, true>(ax, B, it.ref, tb, it.part, it.nparts, seg,
+                                                       scratch, lbits, gbits, overflow);
     // publish this partition's first-touch words (one atomic per non-zero word)
     const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)prod[row] + 31) / 32);
     for (int64_t w = threadIdx.x; w < W; w += TEAM)
@@ -210,10 +284,10 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(Rows A, Rows B, const un
 }
 
 // Exclusive popcount prefix of each partitioned row's first-touch bitmap.
-__global__ __launch_bounds__(256) void k_bitmap_prefix(const int32_t *list, int32_t count,
+__global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32_t count,
                                                        const int32_t *prod, Bitmap bm) {
     __shared__ int scratch[8];
-    const int64_t row = list[blockIdx.x];
+    const int64_t row = list[blockIdx.x].row;
     const int64_t W = (prod[row] + 31) / 32;
     const uint32_t *bits = bm.bits + bm.off[row];
     uint32_t *pref = bm.pref + bm.off[row];
@@ -229,56 +303,70 @@ __global__ __launch_bounds__(256) void k_bitmap_prefix(const int32_t *list, int3
 }
 
 // ---------------------------------------------------------------- numeric kernels
+// Value bins: LDS layout per team [vals 8S | keys 4S | meta 4S | segment | scratch].
 template <int TEAM, int K, int SEG, int TPW, int PER>
-__global__ __launch_bounds__(TEAM *TPW) void k_numeric_lds(Rows A, Rows B, const int32_t *list,
+__global__ __launch_bounds__(TEAM *TPW) void k_numeric_val(AxView ax, Rows B, const RowRef *list,
                                                             int32_t count, uint32_t S, Out out) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    unsigned char *base = smem + (size_t)team * num_team_bytes<SEG>(S);
+    unsigned char *base = smem + (size_t)team * val_team_bytes<SEG>(S);
     double *vals = (double *)base;
     int32_t *keys = (int32_t *)(base + round16(8ull * S));
     uint32_t *meta = (uint32_t *)(base + round16(8ull * S) + round16(4ull * S));
     unsigned char *fixed = base + round16(8ull * S) + 2 * round16(4ull * S);
     auto &seg = *(Seg<SEG, true> *)fixed;
     int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, true>)));
-    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx] : -1;
+    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
     NumTable<false> tb{keys, meta, vals, S};
-    numeric_row<TEAM, K, SEG, false, false, PER>(A, B, row, tb, 0, 1, nullptr, nullptr, seg, scratch,
-                                                  out, 0, nullptr);
+    numeric_row<TEAM, K, SEG, M_VAL, PER>(ax, B, ref, tb, 0, 1, nullptr, nullptr, seg, scratch, out,
+                                          nullptr);
 }
 
+// Direct-write bins: LDS layout per team [keys 4S | meta 4S | segment | scratch].
+template <int TEAM, int K, int SEG, int TPW>
+__global__ __launch_bounds__(TEAM *TPW) void k_numeric_dw(AxView ax, Rows B, const RowRef *list,
+                                                           int32_t count, uint32_t S, Out out) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    unsigned char *base = smem + (size_t)team * dw_team_bytes<SEG>(S);
+    int32_t *keys = (int32_t *)base;
+    uint32_t *meta = (uint32_t *)(base + round16(4ull * S));
+    unsigned char *fixed = base + 2 * round16(4ull * S);
+    auto &seg = *(Seg<SEG, true> *)fixed;
+    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, true>)));
+    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
+    NumTable<false> tb{keys, meta, nullptr, S};
+    numeric_row<TEAM, K, SEG, M_DW, 1>(ax, B, ref, tb, 0, 1, nullptr, nullptr, seg, scratch, out,
+                                       nullptr);
+}
+
+// One workgroup per (row, hash partition), direct write, ranks from the bitmap.
 template <int TEAM, int K, int LOG2S, int SEG>
-__global__ __launch_bounds__(TEAM) void k_numeric_part(Rows A, Rows B, const unsigned long long *items,
-                                                       const int32_t *nnz_row, int32_t part_cap,
+__global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const PartItem *items,
                                                        Bitmap bm, Out out, int *overflow) {
     __shared__ int32_t keys[1 << LOG2S];
     __shared__ uint32_t meta[1 << LOG2S];
-    __shared__ double vals[1 << LOG2S];
     __shared__ Seg<SEG, true> seg;
     __shared__ int scratch[64];
-    const unsigned long long it = items[blockIdx.x];
-    const int64_t row = (int64_t)(it >> 32);
-    const uint32_t part = (uint32_t)(it & 0xFFFFFFFFu);
-    const int32_t nnz = nnz_row[row];
-    const uint32_t np = nparts_of(nnz, part_cap);
-    NumTable<false> tb{keys, meta, vals, 1u << LOG2S};
-    numeric_row<TEAM, K, SEG, false, true, 1>(A, B, row, tb, part, np, bm.bits + bm.off[row],
-                                              bm.pref + bm.off[row], seg, scratch, out, nnz, overflow);
+    const PartItem it = items[blockIdx.x];
+    const int64_t row = it.ref.row;
+    NumTable<false> tb{keys, meta, nullptr, 1u << LOG2S};
+    numeric_row<TEAM, K, SEG, M_DWPART, 1>(ax, B, it.ref, tb, it.part, it.nparts, bm.bits + bm.off[row],
+                                           bm.pref + bm.off[row], seg, scratch, out, overflow);
 }
 
 template <int TEAM, int K, int SEG>
-__global__ __launch_bounds__(TEAM) void k_numeric_global(Rows A, Rows B, const int32_t *list,
-                                                         const int64_t *ws_off,
-                                                         const int32_t *nnz_row, int32_t count,
+__global__ __launch_bounds__(TEAM) void k_numeric_global(AxView ax, Rows B, const RowRef *list,
+                                                         const int64_t *ws_off, int32_t count,
                                                          char *ws, Out out) {
     __shared__ Seg<SEG, true> seg;
     __shared__ int scratch[64];
     const int64_t idx = blockIdx.x;
     if (idx >= count) return;
-    const int64_t row = list[idx];
-    const unsigned long long k = (unsigned long long)nnz_row[row];
+    const RowRef ref = list[idx];
+    const unsigned long long k = (unsigned long long)out.len[ref.row];
     const unsigned long long need = k + (k + 1) / 2;
     uint32_t l2 = 0;
     while ((1ull << l2) < need) ++l2;
@@ -287,8 +375,8 @@ __global__ __launch_bounds__(TEAM) void k_numeric_global(Rows A, Rows B, const i
     char *base = ws + (uint64_t)ws_off[idx] * 20ull;
     NumTable<true> tb{(int32_t *)base, (unsigned long long *)(base + S * 4ull),
                       (double *)(base + S * 12ull), (uint32_t)S};
-    numeric_row<TEAM, K, SEG, true, false, 1>(A, B, row, tb, 0, 1, nullptr, nullptr, seg, scratch,
-                                              out, 0, nullptr);
+    numeric_row<TEAM, K, SEG, M_WIDE, 1>(ax, B, ref, tb, 0, 1, nullptr, nullptr, seg, scratch, out,
+                                         nullptr);
 }
 
 // ---------------------------------------------------------------- scan
@@ -444,7 +532,7 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
 }
 
 template <int TEAM, int CAP, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const int32_t *list, int32_t count,
+__global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const RowRef *list, int32_t count,
                                                          const int64_t *ptr, const int32_t *len,
                                                          int64_t stride, int32_t *col, double *val) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
@@ -453,7 +541,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const int32_t *list, int
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
     const int lane = Team<TEAM>::lane();
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx] : -1;
+    const int64_t row = idx < count ? list[idx].row : -1;
     int64_t o = 0;
     int32_t n = 0;
     if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
@@ -469,13 +557,13 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const int32_t *list, int
     }
 }
 
-__global__ __launch_bounds__(1024) void k_sort_global(const int32_t *list, int32_t count,
+__global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_t count,
                                                       const int64_t *ws_off, const int64_t *ptr,
                                                       const int32_t *len, int64_t stride,
                                                       int32_t *col, double *val, char *ws) {
     const int64_t idx = blockIdx.x;
     if (idx >= count) return;
-    const int64_t row = list[idx];
+    const int64_t row = list[idx].row;
     int64_t o;
     int32_t n;
     sort_row_span(ptr, len, stride, row, o, n);
@@ -507,50 +595,67 @@ __global__ void k_row_len(const int64_t *ptr, int64_t rows, int32_t *len) {
 using namespace ias;
 using namespace ias::dev;
 
-// Bin tables.  Symbolic bins by products, keys-only LDS tables
-// at load <= 2/3; rows beyond 5460 products are hash-partitioned (4096
-// products per partition, 8192-slot key+first-touch tables) and get a
-// first-touch bitmap.  Numeric bins by nnz with 16-byte slots; rows beyond
-// 5460 nnz are hash-partitioned (4096 per partition); rows at >= 2^19 - 1 nnz
-// (beyond the 19-bit rank field) use a per-row table in global memory.
+// Bin tables.
+//  * Symbolic: rows by products into keys-only LDS tables (load <= 2/3, any
+//    slot count); beyond SYM_MAX products a row is hash-partitioned
+//    (SYM_MAX products per partition) and gets a first-touch bitmap.
+//  * Numeric: rows by nnz.  Rows with many duplicate products (products >
+//    1.5 nnz) and nnz <= VAL_MAX use value tables (16 B/slot, LDS-staged
+//    emission); all others use direct-write tables (8 B/slot) up to DW_MAX;
+//    beyond DW_MAX a row is hash-partitioned (direct write, bitmap ranks);
+//    rows at >= 2^19 - 1 nnz (beyond the 19-bit rank field) use a per-row
+//    table in global memory.  DW_MAX >= SYM_MAX, so every partitioned
+//    numeric row has a bitmap.
 static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-constexpr int32_t LDS_MAX = 5460;
-constexpr int32_t PART_CAP = 4096;
+constexpr int32_t SYM_MAX = 10922;
+constexpr int32_t VAL_MAX = 5460;
+constexpr int32_t DW_MAX = 10922;
+constexpr int32_t SYM_PART_CAP = 10922;   // products per symbolic partition (16384-slot table)
+constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
+static_assert(DW_MAX >= SYM_MAX, "numeric partitions need the symbolic bitmap");
 
-// LDS bins: upper bound of the key (products for symbolic, nnz for numeric),
-// kernel configuration, and table slots S = ceil(1.5 * upper).
+// LDS bins: upper bound of the key and kernel configuration; table slots
+// S = ceil(1.5 * upper).
 struct BinCfg {
     int32_t upper;
     int32_t cfg;
 };
-static constexpr BinCfg SYM_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {1024, 4}, {1536, 5},
-                                   {2048, 5}, {2730, 5}, {3640, 6}, {4550, 6}, {LDS_MAX, 6}};
-static constexpr BinCfg NUM_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
-                                   {512, 4},  {768, 5},  {1024, 5}, {1365, 5}, {1820, 6},
-                                   {2430, 6}, {3240, 7}, {4320, 7}, {LDS_MAX, 7}};
-constexpr int N_SYM_BINS = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
-constexpr int N_NUM_BINS = sizeof(NUM_BINS) / sizeof(NUM_BINS[0]);
-static_assert(N_NUM_BINS + 3 <= MAX_BINS, "bins");
+static constexpr BinCfg SYM_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {1024, 4},
+                                      {1536, 5}, {2048, 5}, {2730, 5}, {3640, 6}, {4550, 6},
+                                      {5460, 6}, {7280, 7}, {9100, 7}, {SYM_MAX, 7}};
+static constexpr BinCfg VAL_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
+                                      {512, 4},  {768, 5},  {1024, 5}, {1365, 5}, {1820, 6},
+                                      {2430, 6}, {3240, 7}, {4320, 7}, {VAL_MAX, 7}};
+static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},   {256, 3},
+                                     {512, 4},  {768, 5},  {1024, 5}, {1536, 6},  {2048, 6},
+                                     {3072, 7}, {4096, 7}, {6144, 7}, {8192, 7},  {DW_MAX, 7}};
+constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
+constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
+constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
+static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 3 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
 
-// TEAM * PER of each numeric configuration in num_bin(): the emission loop
+// TEAM * PER of each value configuration in val_bin(): the emission loop
 // visits that many slots, so it must cover every bin's S.
-static constexpr uint32_t NUM_CFG_EMIT[] = {48, 96, 192, 384, 768, 2048, 4096, 8192};
-static constexpr bool num_bins_covered() {
-    for (int i = 0; i < N_NUM_BINS; ++i)
-        if (NUM_CFG_EMIT[NUM_BINS[i].cfg] < slots_for(NUM_BINS[i].upper)) return false;
+static constexpr uint32_t VAL_CFG_EMIT[] = {48, 96, 192, 384, 768, 2048, 4096, 8192};
+static constexpr bool val_bins_covered() {
+    for (int i = 0; i < N_VAL; ++i)
+        if (VAL_CFG_EMIT[VAL_BINS[i].cfg] < slots_for(VAL_BINS[i].upper)) return false;
     return true;
 }
-static_assert(num_bins_covered(), "numeric emission does not cover a bin's table");
+static_assert(val_bins_covered(), "value-bin emission does not cover a bin's table");
 
 static BinSpec sym_spec() {
     BinSpec s{};
-    s.nlds = N_SYM_BINS;
-    for (int i = 0; i < N_SYM_BINS; ++i) s.upper[i + 1] = SYM_BINS[i].upper;
-    s.part_cap = PART_CAP;
+    s.nval = N_SYM;
+    s.ndw = 0;
+    for (int i = 0; i < N_SYM; ++i) s.upper[i + 1] = SYM_BINS[i].upper;
+    s.ratio_num = 0;
+    s.ratio_den = 0;
+    s.part_cap = SYM_PART_CAP;
     s.wide_min = 0;
     s.ft = 1;
     s.zero_nnz = 1;
@@ -559,70 +664,113 @@ static BinSpec sym_spec() {
 
 static BinSpec num_spec() {
     BinSpec s{};
-    s.nlds = N_NUM_BINS;
-    for (int i = 0; i < N_NUM_BINS; ++i) s.upper[i + 1] = NUM_BINS[i].upper;
-    s.part_cap = PART_CAP;
+    s.nval = N_VAL;
+    s.ndw = N_DW;
+    for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
+    for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
+    s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
+    s.ratio_den = 2;
+    s.part_cap = NUM_PART_CAP;
     s.wide_min = WIDE_MIN;
     s.ft = 0;
     s.zero_nnz = 0;
     return s;
 }
 
-// Allow up to the full 160 KiB of LDS for a dynamically sized kernel (once).
+// Dynamic LDS beyond 64 KiB is requested per kernel (once per instantiation:
+// the callers below are templates, so each has its own flag).
 template <typename F>
-static void allow_lds(F kernel) {
-    static bool done = false;
-    if (!done) {
+static void allow_lds(F kernel, bool &done, size_t bytes) {
+    if (!done && bytes > 65536) {
         hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipGetLastError();   // a refusal shows up at launch
         done = true;
     }
 }
 
+struct Launch {
+    int c;
+    uint32_t S;
+    hipStream_t s;
+    const AxView &ax;
+    const Rows &B;
+    const RowRef *list;
+};
+
 template <int TEAM, int K, int SEG, int TPW>
-static void sym_launch(int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B, const int32_t *list,
-                       int32_t *nnz) {
+static void sym_launch(const Launch &l, int32_t *nnz) {
     auto kern = k_symbolic_lds<TEAM, K, SEG, TPW>;
-    allow_lds(kern);
-    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(S);
-    kern<<<grid_for(c, TPW), TEAM * TPW, lds, s>>>(A, B, list, c, S, nnz);
+    static bool done = false;
+    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(l.S);
+    allow_lds(kern, done, lds);
+    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, nnz);
 }
 
-static void sym_bin(int cfg, int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B,
-                    const int32_t *list, int32_t *nnz) {
+static void sym_bin(int cfg, const Launch &l, int32_t *nnz) {
     switch (cfg) {
-        case 0: sym_launch<16, 4, 16, 16>(c, S, s, A, B, list, nnz); break;
-        case 1: sym_launch<32, 4, 32, 8>(c, S, s, A, B, list, nnz); break;
-        case 2: sym_launch<64, 4, 64, 4>(c, S, s, A, B, list, nnz); break;
-        case 3: sym_launch<64, 8, 64, 4>(c, S, s, A, B, list, nnz); break;
-        case 4: sym_launch<128, 8, 128, 1>(c, S, s, A, B, list, nnz); break;
-        case 5: sym_launch<256, 8, 256, 1>(c, S, s, A, B, list, nnz); break;
-        default: sym_launch<512, 8, 256, 1>(c, S, s, A, B, list, nnz); break;
+        case 0: sym_launch<16, 4, 16, 16>(l, nnz); break;
+        case 1: sym_launch<32, 4, 32, 8>(l, nnz); break;
+        case 2: sym_launch<64, 4, 64, 4>(l, nnz); break;
+        case 3: sym_launch<64, 8, 64, 4>(l, nnz); break;
+        case 4: sym_launch<128, 8, 128, 1>(l, nnz); break;
+        case 5: sym_launch<256, 8, 256, 1>(l, nnz); break;
+        case 6: sym_launch<512, 8, 256, 1>(l, nnz); break;
+        default: sym_launch<1024, 4, 256, 1>(l, nnz); break;
     }
 }
 
 template <int TEAM, int K, int SEG, int TPW, int PER>
-static void num_launch(int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B, const int32_t *list,
-                       const Out &out) {
-    auto kern = k_numeric_lds<TEAM, K, SEG, TPW, PER>;
-    allow_lds(kern);
-    const size_t lds = (size_t)TPW * num_team_bytes<SEG>(S);
-    kern<<<grid_for(c, TPW), TEAM * TPW, lds, s>>>(A, B, list, c, S, out);
+static void val_launch(const Launch &l, const Out &out) {
+    auto kern = k_numeric_val<TEAM, K, SEG, TPW, PER>;
+    static bool done = false;
+    const size_t lds = (size_t)TPW * val_team_bytes<SEG>(l.S);
+    allow_lds(kern, done, lds);
+    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, out);
 }
 
-static void num_bin(int cfg, int c, uint32_t S, hipStream_t s, const Rows &A, const Rows &B,
-                    const int32_t *list, const Out &out) {
+static void val_bin(int cfg, const Launch &l, const Out &out) {
     switch (cfg) {
-        case 0: num_launch<16, 4, 16, 16, 3>(c, S, s, A, B, list, out); break;
-        case 1: num_launch<32, 4, 32, 8, 3>(c, S, s, A, B, list, out); break;
-        case 2: num_launch<64, 4, 64, 4, 3>(c, S, s, A, B, list, out); break;
-        case 3: num_launch<64, 4, 64, 2, 6>(c, S, s, A, B, list, out); break;
-        case 4: num_launch<128, 4, 128, 1, 6>(c, S, s, A, B, list, out); break;
-        case 5: num_launch<256, 4, 256, 1, 8>(c, S, s, A, B, list, out); break;
-        case 6: num_launch<512, 4, 256, 1, 8>(c, S, s, A, B, list, out); break;
-        default: num_launch<1024, 2, 256, 1, 8>(c, S, s, A, B, list, out); break;
+        case 0: val_launch<16, 4, 16, 16, 3>(l, out); break;
+        case 1: val_launch<32, 4, 32, 8, 3>(l, out); break;
+        case 2: val_launch<64, 4, 64, 4, 3>(l, out); break;
+        case 3: val_launch<64, 4, 64, 2, 6>(l, out); break;
+        case 4: val_launch<128, 4, 128, 1, 6>(l, out); break;
+        case 5: val_launch<256, 4, 256, 1, 8>(l, out); break;
+        case 6: val_launch<512, 4, 256, 1, 8>(l, out); break;
+        default: val_launch<1024, 2, 256, 1, 8>(l, out); break;
     }
 }
 
+template <int TEAM, int K, int SEG, int TPW>
+static void dw_launch(const Launch &l, const Out &out) {
+    auto kern = k_numeric_dw<TEAM, K, SEG, TPW>;
+    static bool done = false;
+    const size_t lds = (size_t)TPW * dw_team_bytes<SEG>(l.S);
+    allow_lds(kern, done, lds);
+    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, out);
+}
+
+static void dw_bin(int cfg, const Launch &l, const Out &out) {
+    switch (cfg) {
+        case 0: dw_launch<16, 4, 16, 16>(l, out); break;
+        case 1: dw_launch<32, 4, 32, 8>(l, out); break;
+        case 2: dw_launch<64, 4, 64, 4>(l, out); break;
+        case 3: dw_launch<64, 4, 64, 2>(l, out); break;
+        case 4: dw_launch<128, 4, 128, 1>(l, out); break;
+        case 5: dw_launch<256, 4, 256, 1>(l, out); break;
+        case 6: dw_launch<512, 4, 256, 1>(l, out); break;
+        default: dw_launch<1024, 2, 256, 1>(l, out); break;
+    }
+}
+
+// start of each bin's compact list (bins in numeric order; bin 0 unlisted)
+static void bin_starts(const Counters &c, int64_t *start) {
+    int64_t acc = 0;
+    for (int i = 0; i < MAX_BINS; ++i) {
+        start[i] = acc;
+        acc += i > 0 ? c.count[i] : 0;
+    }
+}
 
 #define HIPC(x)                                                                   \
     do {                                                                          \
@@ -631,6 +779,27 @@ static void num_bin(int cfg, int c, uint32_t S, hipStream_t s, const Rows &A, co
             set_last_error("%s failed: %s", #x, hipGetErrorString(_e));           \
             return _e == hipErrorOutOfMemory ? IAS_ERROR_OUT_OF_MEMORY : IAS_ERROR_DEVICE; \
         }                                                                         \
+    } while (0)
+
+// IAS_DEBUG_SYNC=1: synchronise and check after every launch group, naming
+// the group in ias_last_error() (diagnostics only; off by default).
+static bool debug_sync() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_DEBUG_SYNC");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+#define CHECK_LAUNCH(what, strm)                                                          \
+    do {                                                                                 \
+        if (debug_sync()) {                                                              \
+            hipError_t _e = hipGetLastError();                                           \
+            if (_e == hipSuccess) _e = hipStreamSynchronize(strm);                       \
+            if (_e != hipSuccess) {                                                      \
+                set_last_error("%s: %s", what, hipGetErrorString(_e));                   \
+                return IAS_ERROR_DEVICE;                                                 \
+            }                                                                            \
+        }                                                                                \
     } while (0)
 
 ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
@@ -675,17 +844,25 @@ ias_status ias_plan::init(int dev, void *strm) {
 template <typename T>
 static T *as(ias_plan::Buf &b) { return (T *)b.p; }
 
+AxView ias_plan::ax_view() {
+    return AxView{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), as<double>(bufs[B_AXV])};
+}
+
 ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
-                              ias_report *rep) {
+                              int64_t a_entries, ias_report *rep) {
     (void)cols;
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
     const BinSpec ss = sym_spec(), ns = num_spec();
+    const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
+    IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
+    IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
+    IAS_TRY(reserve(B_AXV, sizeof(double) * ae));
     IAS_TRY(reserve(B_PROD, sizeof(int32_t) * (rows + 1)));
     IAS_TRY(reserve(B_NNZ, sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(reserve(B_SLIST, sizeof(int32_t) * rows * MAX_BINS + 4));
-    IAS_TRY(reserve(B_NLIST, sizeof(int32_t) * rows * MAX_BINS + 4));
+    IAS_TRY(reserve(B_SLIST, sizeof(RowRef) * (rows + 1)));
+    IAS_TRY(reserve(B_NLIST, sizeof(RowRef) * (rows + 1)));
     IAS_TRY(reserve(B_BMOFF, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(reserve(B_WSOFF, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(reserve(B_CNT, sizeof(Counters)));
@@ -696,69 +873,78 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT2]);
     Counters *hc = (Counters *)host_counters;
+    const AxView ax = ax_view();
 
-    // ---- analysis + binning by products
+    // ---- analysis: products per row, expanded A, symbolic bin counts
     HIPC(hipEventRecord(ev[0], s));
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     HIPC(hipMemsetAsync(dc2, 0, sizeof(Counters), s));
-    // items worst case: every row partitioned -> sum of ceil(P/cap) <= rows + flops/cap;
-    // bounded below after the counters are read (the kernel writes at most that many).
-    if (rows > 0) {
+    if (rows > 0)
         k_row_products<<<grid_for(rows, AN_BLOCK), AN_BLOCK, 0, s>>>(
-            A, B, rows, as<int32_t>(bufs[B_PROD]), &dc->flops, &dc->max_prod);
-        HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
-        flops = (int64_t)hc->flops;
-        max_prod = hc->max_prod;
-        IAS_TRY(reserve(B_SITEM, sizeof(unsigned long long) * (size_t)(rows + flops / PART_CAP + 2)));
-        k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            as<int32_t>(bufs[B_PROD]), rows, ss, as<int32_t>(bufs[B_SLIST]),
-            as<unsigned long long>(bufs[B_SITEM]), as<int64_t>(bufs[B_BMOFF]),
-            as<int64_t>(bufs[B_WSOFF]), as<int32_t>(bufs[B_NNZ]), dc);
-    } else {
-        flops = 0;
-        max_prod = 0;
-    }
-    HIPC(hipEventRecord(ev[1], s));
+            A, B, rows, AxOut{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), as<double>(bufs[B_AXV])},
+            a_entries, as<int32_t>(bufs[B_PROD]), ss, dc);
+    CHECK_LAUNCH("k_row_products", s);
+    HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
+    if (c1.overflow) {
+        set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
+        return IAS_ERROR_INVALID_ARGUMENT;
+    }
+    flops = (int64_t)c1.flops;
+    max_prod = c1.max_prod;
 
-    // ---- symbolic
-    const int32_t *L = as<int32_t>(bufs[B_SLIST]);
-    int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
-    auto lst = [&](int b) { return L + (int64_t)b * rows; };
+    // ---- symbolic binning + symbolic
+    IAS_TRY(reserve(B_SITEM, sizeof(PartItem) * (size_t)(c1.items + 1)));
+    const int sym_part = ss.nval + 1;
     Bitmap bm{nullptr, nullptr, as<int64_t>(bufs[B_BMOFF])};
-    if (c1.count[ss.nlds + 1] > 0) {
+    if (c1.count[sym_part] > 0) {
         IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
         IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
         bm.bits = as<uint32_t>(bufs[B_BITS]);
         bm.pref = as<uint32_t>(bufs[B_BPREF]);
         HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
     }
+    RowRef *SL = as<RowRef>(bufs[B_SLIST]);
+    int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
+    if (rows > 0)
+        k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
+            as<int32_t>(bufs[B_PROD]), nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
+            as<int64_t>(bufs[B_BMOFF]), nullptr, nnz, dc);
+    CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
+    HIPC(hipEventRecord(ev[1], s));
+    int64_t st[MAX_BINS];
+    bin_starts(c1, st);
     int c;
-    for (int b = 1; b <= ss.nlds; ++b)
+    for (int b = 1; b <= ss.nval; ++b)
         if ((c = c1.count[b]) > 0)
-            sym_bin(SYM_BINS[b - 1].cfg, c, slots_for(SYM_BINS[b - 1].upper), s, A, B, lst(b), nnz);
-    if ((c = c1.count[ss.nlds + 1]) > 0) {
-        k_symbolic_part<512, 4, 13, 256><<<(unsigned)c1.items, 512, 0, s>>>(
-            A, B, as<unsigned long long>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), PART_CAP, bm, nnz,
-            &dc2->overflow);
-        k_bitmap_prefix<<<c, 256, 0, s>>>(lst(ss.nlds + 1), c, as<int32_t>(bufs[B_PROD]), bm);
+            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(SYM_BINS[b - 1].upper), s, ax, B, SL + st[b]}, nnz);
+    CHECK_LAUNCH("k_symbolic_lds", s);
+    if ((c = c1.count[sym_part]) > 0) {
+        k_symbolic_part<1024, 4, 14, 256><<<(unsigned)c1.items, 1024, 0, s>>>(
+            ax, B, as<PartItem>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), bm, nnz, &dc2->overflow);
+    CHECK_LAUNCH("k_symbolic_part", s);
+        k_bitmap_prefix<<<c, 256, 0, s>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+        CHECK_LAUNCH("k_bitmap_prefix", s);
     }
     HIPC(hipGetLastError());
 
-    // ---- row pointer of C, numeric binning by nnz
+    // ---- row pointer of C, numeric binning by nnz (and products / nnz)
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
+    IAS_TRY(reserve(B_NITEM, sizeof(PartItem) * (size_t)(rows + flops / NUM_PART_CAP + 2)));
     if (rows > 0) {
         k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
                                                           &dc2->max_nnz);
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART]), nb);
         k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
-        IAS_TRY(reserve(B_NITEM, sizeof(unsigned long long) * (size_t)(rows + flops / PART_CAP + 2)));
-        k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            nnz, rows, ns, as<int32_t>(bufs[B_NLIST]), as<unsigned long long>(bufs[B_NITEM]), nullptr,
-            as<int64_t>(bufs[B_WSOFF]), nullptr, dc2);
+    CHECK_LAUNCH("scan", s);
+        k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), rows,
+                                                                    ns, dc2);
+        k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
+            nnz, as<int32_t>(bufs[B_PROD]), rows, ns, A, as<RowRef>(bufs[B_NLIST]),
+            as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, dc2);
+    CHECK_LAUNCH("numeric binning", s);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
     }
@@ -790,30 +976,45 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     return IAS_SUCCESS;
 }
 
-ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out, ias_report *rep) {
+ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ias_report *rep) {
+    (void)A;
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     const int64_t rows = n_rows;
     const BinSpec ns = num_spec();
-    const int part_bin = ns.nlds + 1, wide_bin = ns.nlds + 2;
+    const int part_bin = ns.nval + 1, wide_bin = ns.nval + 2;
     if (num_count[wide_bin] > 0) IAS_TRY(reserve(B_WS, 20ull * num_ws));
-    const int32_t *L = as<int32_t>(bufs[B_NLIST]);
-    auto lst = [&](int b) { return L + (int64_t)b * rows; };
+    Out out = out_in;
+    out.len = as<int32_t>(bufs[B_NNZ]);
+    const RowRef *NL = as<RowRef>(bufs[B_NLIST]);
+    Counters cc{};
+    std::copy(num_count, num_count + MAX_BINS, cc.count);
+    int64_t st[MAX_BINS];
+    bin_starts(cc, st);
     Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    const AxView ax = ax_view();
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     HIPC(hipEventRecord(ev[3], s));
     int c;
-    for (int b = 1; b <= ns.nlds; ++b)
-        if ((c = num_count[b]) > 0)
-            num_bin(NUM_BINS[b - 1].cfg, c, slots_for(NUM_BINS[b - 1].upper), s, A, B, lst(b), out);
+    // big bins first: their long rows start early and the small bins fill in behind
     if (num_count[part_bin] > 0)
-        k_numeric_part<1024, 2, 13, 256><<<(unsigned)num_items, 1024, 0, s>>>(
-            A, B, as<unsigned long long>(bufs[B_NITEM]), as<int32_t>(bufs[B_NNZ]), PART_CAP, bm, out,
-            &dc2->overflow);
+        k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, s>>>(
+            ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
+    CHECK_LAUNCH("k_numeric_part", s);
     if ((c = num_count[wide_bin]) > 0)
-        k_numeric_global<1024, 2, 256><<<c, 1024, 0, s>>>(A, B, lst(wide_bin), as<int64_t>(bufs[B_WSOFF]),
-                                                          as<int32_t>(bufs[B_NNZ]), c,
-                                                          (char *)bufs[B_WS].p, out);
+        k_numeric_global<1024, 2, 256><<<c, 1024, 0, s>>>(ax, B, NL + st[wide_bin], as<int64_t>(bufs[B_WSOFF]),
+                                                          c, (char *)bufs[B_WS].p, out);
+    CHECK_LAUNCH("k_numeric_global", s);
+    for (int i = N_DW - 1; i >= 0; --i) {
+        const int b = ns.nval + 3 + i;
+        if ((c = num_count[b]) > 0)
+            dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), s, ax, B, NL + st[b]}, out);
+        CHECK_LAUNCH("k_numeric_dw", s);
+    }
+    for (int b = ns.nval; b >= 1; --b)
+        if ((c = num_count[b]) > 0)
+            val_bin(VAL_BINS[b - 1].cfg, Launch{c, slots_for(VAL_BINS[b - 1].upper), s, ax, B, NL + st[b]}, out);
+    CHECK_LAUNCH("k_numeric_val", s);
     if (out.row_idx && rows > 0)
         k_fill_rows<<<grid_for(rows * WAVE, 256), 256, 0, s>>>(out.ptr, rows, out.row_idx);
     HIPC(hipGetLastError());
@@ -845,7 +1046,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     hipStream_t s = (hipStream_t)plan->stream;
     HIPC(hipSetDevice(plan->device));
     IAS_TRY(plan->reserve(ias_plan::B_TMP0, sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(plan->reserve(ias_plan::B_TMP1, sizeof(int32_t) * rows * MAX_BINS + 4));
+    IAS_TRY(plan->reserve(ias_plan::B_TMP1, sizeof(RowRef) * (rows + 1)));
     IAS_TRY(plan->reserve(ias_plan::B_TMP2, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(plan->reserve(ias_plan::B_TMP3, sizeof(Counters)));
     const int32_t *len = len_in;
@@ -856,22 +1057,27 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     BinSpec spec{};
-    spec.nlds = 6;
+    spec.nval = 6;
     const int32_t u[] = {0, 32, 128, 512, 2048, 4096, 8192};
     for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
     spec.wide_min = 8193;   // everything beyond the LDS bins -> global workspace
-    int32_t *lists = (int32_t *)plan->bufs[ias_plan::B_TMP1].p;
+    RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
-    k_bin_rows<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, rows, spec, lists, nullptr, nullptr,
-                                                                offs, nullptr, dc);
+    // the scatter's row extents are not used by the sort kernels (they read ptr/len)
+    const Rows span{ptr, len, stride, nullptr, nullptr};
+    k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, rows, spec, dc);
+    k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, rows, spec, span, lists,
+                                                                  nullptr, nullptr, offs, nullptr, dc);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    const int wide = spec.nlds + 2;
+    const int wide = spec.nval + 2;
     if (hc.count[wide] > 0)
         IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
-    auto lst = [&](int b) { return lists + (int64_t)b * rows; };
+    int64_t st[MAX_BINS];
+    bin_starts(hc, st);
+    auto lst = [&](int b) { return lists + st[b]; };
     int c;
     if ((c = hc.count[1]) > 0)
         k_sort_lds<32, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);

@@ -8,15 +8,19 @@
 
 namespace ias {
 
-constexpr int MAX_BINS = 18;   // 0 = empty rows, 1..nlds = LDS bins, nlds+1 = hash
-                               // partitions, nlds+2 = global-memory table
+constexpr int MAX_BINS = 36;   // 0 = nothing to do, 1..nval = LDS (value) bins, nval+1 =
+                               // hash partitions, nval+2 = global-memory table,
+                               // nval+3.. = direct-write LDS bins
 
 // How a pass bins its rows by `key` (products or nnz).
 struct BinSpec {
-    int32_t nlds;              // LDS bins 1..nlds cover key <= upper[nlds]
-    int32_t upper[MAX_BINS];
-    int32_t part_cap;          // keys per hash partition in bin nlds+1
-    int32_t wide_min;          // key >= wide_min -> bin nlds+2 (0: never)
+    int32_t nval;              // value bins 1..nval cover key <= upper[nval]
+    int32_t ndw;               // direct-write bins nval+3 .. nval+2+ndw
+    int32_t upper[MAX_BINS];   // per LDS bin, indexed by bin number
+    int32_t ratio_num;         // value class iff prod * ratio_den > key * ratio_num
+    int32_t ratio_den;         //   (ratio_den == 0: every row is value class)
+    int32_t part_cap;          // keys per hash partition in bin nval+1
+    int32_t wide_min;          // key >= wide_min -> bin nval+2 (0: never)
     int32_t ft;                // give partitioned rows a first-touch bitmap
     int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
 };
@@ -27,18 +31,20 @@ struct Counters {
     unsigned long long items;     // (row, partition) work items
     unsigned long long bm_words;  // first-touch bitmap words
     unsigned long long ws_slots;  // global-table slots
+    unsigned long long items_cur, bm_cur, ws_cur;   // scatter-pass cursors
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
     int32_t pad;
-    int32_t count[MAX_BINS];
+    int32_t count[MAX_BINS];      // rows per bin (counting pass)
+    int32_t cursor[MAX_BINS];     // scatter-pass cursors
 };
 
 }  // namespace ias
 
 struct ias_plan {
     enum {
-        B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
+        B_AXS, B_AXL, B_AXV, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
     };
@@ -69,8 +75,10 @@ struct ias_plan {
     ias_status init(int device, void *stream);
     ias_status reserve(void **buf, size_t *cap, size_t bytes);
     ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
+    // a_entries: stored entries of A (CSR: nnz of the view; ELL: rows * width)
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
-                        int64_t cols, ias_report *rep);
+                        int64_t cols, int64_t a_entries, ias_report *rep);
+    ias::dev::AxView ax_view();
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
 };

@@ -40,7 +40,7 @@ constexpr int32_t EMPTY_KEY = -1;
 #endif
 
 // ---------------------------------------------------------------- row views
-// A "rows" operand: CSR (ptr != nullptr) or ELL (start = i*stride, len[i]).
+// An operand's rows: CSR (ptr != nullptr) or ELL (start = i*stride, len[i]).
 struct Rows {
     const int64_t *ptr;
     const int32_t *len;
@@ -56,17 +56,49 @@ struct Rows {
             n = len[i];
         }
     }
+    __device__ __forceinline__ int64_t base() const { return ptr ? ptr[0] : 0; }
 };
 
-// Where row i of C goes: CSR/COO (start = ptr[i]) or ELL (start = i*stride).
+// Expanded A, written once by the analysis pass: for every stored A entry
+// q (relative to the first entry of A), the extent of the B row it selects
+// and its value.  The row kernels read only these arrays and B, so a row
+// costs one dependent gather (B) after its work item instead of three
+// (A row pointer, A column, B row pointer).
+struct AxView {
+    const int64_t *bstart;
+    const int32_t *blen;
+    const double *aval;
+};
+struct AxOut {
+    int64_t *bstart;
+    int32_t *blen;
+    double *aval;
+};
+
+// A row of a bin list: its first expanded-A entry and entry count.
+struct RowRef {
+    int64_t q0;
+    int32_t row;
+    int32_t n;
+};
+// One hash partition of a partitioned row.
+struct PartItem {
+    RowRef ref;
+    uint32_t part;
+    uint32_t nparts;
+};
+
+// Where row i of C goes: CSR/COO (start = ptr[i]) or ELL (start = i*stride);
+// len[i] = nnz of row i (from the symbolic pass).
 struct Out {
     const int64_t *ptr;   // C row pointer (CSR/COO); nullptr for ELL
     int64_t stride;       // ELL width
     int32_t *col;
     double *val;
-    int32_t *row_idx;     // COO: row index of every entry (nullable)
+    int32_t *row_idx;     // COO: row index of every entry (nullable; filled by k_fill_rows)
     int32_t order;        // 0: reverse first-touch, 1: forward first-touch
     int32_t first_assign; // 1: first product assigned (COO); 0: 0.0 + product
+    const int32_t *len;   // nnz per row (set by the engine)
     __device__ __forceinline__ int64_t start(int64_t i) const { return ptr ? ptr[i] : i * stride; }
 };
 
@@ -292,26 +324,21 @@ __device__ __forceinline__ int seg_find(const int32_t *pref, int n, int p) {
     return lo;
 }
 
-// Stage A entries [seg0, seg0 + SEG) of row (as, an); returns the products of
-// the segment (team-uniform).  Requires SEG <= TEAM.
+// Stage entries [seg0, seg0 + SEG) of the row's expanded A; returns the
+// products of the segment (team-uniform).  Requires SEG <= TEAM.
 template <int TEAM, int SEG, bool NUMERIC>
-__device__ __forceinline__ int load_segment(const Rows &A, const Rows &B, int64_t as, int32_t an,
-                                            int32_t seg0, Seg<SEG, NUMERIC> &sg, int *scratch,
-                                            int &nseg) {
+__device__ __forceinline__ int load_segment(const AxView &ax, int64_t q0, int32_t an, int32_t seg0,
+                                            Seg<SEG, NUMERIC> &sg, int *scratch, int &nseg) {
     static_assert(SEG <= TEAM, "segment loads one entry per lane");
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     nseg = min(SEG, an - seg0);
     int blen = 0;
     if (lane < nseg) {
-        const int64_t e = as + seg0 + lane;
-        const int32_t j = A.col[e];
-        int64_t bs;
-        int32_t bn;
-        B.row(j, bs, bn);
-        sg.bstart[lane] = bs;
-        if constexpr (NUMERIC) sg.aval[lane] = A.val[e];
-        blen = bn;
+        const int64_t q = q0 + seg0 + lane;
+        sg.bstart[lane] = ax.bstart[q];
+        if constexpr (NUMERIC) sg.aval[lane] = ax.aval[q];
+        blen = ax.blen[q];
     }
     int total;
     const int ex = TM::excl_sum(blen, total, scratch);
@@ -326,7 +353,7 @@ __device__ __forceinline__ int load_segment(const Rows &A, const Rows &B, int64_
 // published as bits of the row's bitmap.  Returns the team's count; *overflow
 // is set when a partition table filled up.
 template <int TEAM, int K, int SEG, bool FT>
-__device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, int64_t row,
+__device__ __forceinline__ int32_t symbolic_row(const AxView &ax, const Rows &B, const RowRef &ref,
                                                 const SymTable<FT> &table, uint32_t part,
                                                 uint32_t nparts, Seg<SEG, false> &sg,
                                                 int *scratch, uint32_t *lbits, uint32_t *gbits,
@@ -339,15 +366,13 @@ __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, in
         if constexpr (FT) table.minp[s] = 0xFFFFFFFFu;
     }
     TM::sync();
-    int64_t as = 0;
-    int32_t an = 0;
-    if (row >= 0) A.row(row, as, an);
+    const int32_t an = ref.n;
     int created = 0;
     bool full = false;
     uint32_t pbase = 0;
     for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
         int nseg;
-        const int P = load_segment<TEAM, SEG, false>(A, B, as, an, seg0, sg, scratch, nseg);
+        const int P = load_segment<TEAM, SEG, false>(ax, ref.q0, an, seg0, sg, scratch, nseg);
         for (int p0 = 0; p0 < P; p0 += TEAM * K) {
             int32_t c[K];
             bool v[K];
@@ -387,17 +412,30 @@ __device__ __forceinline__ int32_t symbolic_row(const Rows &A, const Rows &B, in
 }
 
 // ---------------------------------------------------------------- numeric
-// PART == false: the whole row in one LDS table, ranks from team scans,
-// emission staged through LDS so C is written with coalesced stores.
-// PART == true : hash partition `part` of the row; ranks from the symbolic
-// first-touch bitmap; entries stored straight to their final positions.
-template <int TEAM, int K, int SEG, bool WIDE, bool PART, int PER>
-__device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_t row,
-                                            const NumTable<WIDE> &t, uint32_t part,
+// Modes of a numeric row:
+//   M_VAL   : whole row in one LDS table with values; ranks from team scans;
+//             emission staged through LDS so C is written with coalesced
+//             stores (rows with many duplicate products: values stay in LDS).
+//   M_WIDE  : as M_VAL with the table in global memory (64-bit meta) and
+//             entries stored straight to their final positions.
+//   M_DW    : direct write.  The LDS table holds keys and ranks only (8 B per
+//             slot); a column's first touch writes (col, 0.0 + p) to its final
+//             position in C at once and later products of it accumulate there
+//             in product order.  No emission pass.  For rows whose products
+//             are mostly distinct columns.
+//   M_DWPART: M_DW over hash partition `part` of the row, ranks from the
+//             symbolic first-touch bitmap.
+enum { M_VAL = 0, M_WIDE = 1, M_DW = 2, M_DWPART = 3 };
+
+template <int TEAM, int K, int SEG, int MODE, int PER>
+__device__ __forceinline__ void numeric_row(const AxView &ax, const Rows &B, const RowRef &ref,
+                                            const NumTable<MODE == M_WIDE> &t, uint32_t part,
                                             uint32_t nparts, const uint32_t *bits,
                                             const uint32_t *bpref, Seg<SEG, true> &sg,
-                                            int *scratch, const Out &out, int32_t nnz_row,
-                                            int *overflow) {
+                                            int *scratch, const Out &out, int *overflow) {
+    constexpr bool WIDE = MODE == M_WIDE;
+    constexpr bool DW = MODE == M_DW || MODE == M_DWPART;
+    constexpr bool PART = MODE == M_DWPART;
     using TM = Team<TEAM>;
     using MT = MetaTraits<WIDE>;
     using M = typename MT::T;
@@ -405,20 +443,28 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
                   "item ids must fit the owner field");
     const int lane = TM::lane();
     const uint32_t S = t.size;
+    const int64_t row = ref.row;
     for (uint32_t s = lane; s < S; s += TEAM) {
         t.key[s] = EMPTY_KEY;
         t.meta[s] = MT::INIT;
     }
+    // direct-write modes need the row's place in C up front (loads overlap the gathers)
+    int64_t o = 0;
+    uint32_t nnz = 0;
+    if constexpr (DW) {
+        if (row >= 0) {
+            o = out.start(row);
+            nnz = (uint32_t)out.len[row];
+        }
+    }
     TM::sync();
-    int64_t as = 0;
-    int32_t an = 0;
-    if (row >= 0) A.row(row, as, an);
+    const int32_t an = ref.n;
     uint32_t base_rank = 0;
     uint32_t pbase = 0;
     bool full = false;
     for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
         int nseg;
-        const int P = load_segment<TEAM, SEG, true>(A, B, as, an, seg0, sg, scratch, nseg);
+        const int P = load_segment<TEAM, SEG, true>(ax, ref.q0, an, seg0, sg, scratch, nseg);
         for (int p0 = 0; p0 < P; p0 += TEAM * K) {
             int slot[K];
             double prod[K];
@@ -472,10 +518,10 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
                     win[k] = pend[k] && ((IAS_ABLATE & 1) || (m & MT::OWN) == (M)(k * TEAM + lane));
                     rank[k] = m >> MT::SHIFT;
                 }
-                if (first_round) {
-                    bool ft[K];
+                bool ft[K];
 #pragma unroll
-                    for (int k = 0; k < K; ++k) ft[k] = win[k] && rank[k] == MT::RANK_NONE;
+                for (int k = 0; k < K; ++k) ft[k] = first_round && win[k] && rank[k] == MT::RANK_NONE;
+                if (first_round) {
                     if constexpr (!PART) {
                         int r[K] = {};
                         const int total = (IAS_ABLATE & 8) ? 0 : TM::template excl_count_items<K>(ft, r, scratch);
@@ -491,21 +537,24 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
                                 rank[k] = (M)(bpref[p >> 5] + __popc(bits[p >> 5] & ((1u << (p & 31)) - 1u)));
                             }
                     }
-#pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        if (win[k]) {
-                            const double v = ft[k] ? (out.first_assign ? prod[k] : 0.0 + prod[k])
-                                                   : t.val[slot[k]] + prod[k];
-                            t.val[slot[k]] = v;
-                        }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < K; ++k)
-                        if (win[k]) t.val[slot[k]] = t.val[slot[k]] + prod[k];
                 }
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (win[k]) {
+                        if constexpr (DW) {
+                            const uint32_t r = (uint32_t)rank[k];
+                            const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
+                            if (ft[k]) {
+                                out.col[pos] = c[k];
+                                out.val[pos] = out.first_assign ? prod[k] : 0.0 + prod[k];
+                            } else {
+                                out.val[pos] = out.val[pos] + prod[k];
+                            }
+                        } else {
+                            const double v = ft[k] ? (out.first_assign ? prod[k] : 0.0 + prod[k])
+                                                   : t.val[slot[k]] + prod[k];
+                            t.val[slot[k]] = v;
+                        }
                         t.meta[slot[k]] = (rank[k] << MT::SHIFT) | MT::OWN;
                         pend[k] = false;
                     }
@@ -521,26 +570,26 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
         TM::sync();
     }
     if (full) atomicOr(overflow, 1);
+    if constexpr (DW) return;
     if (row < 0 || (IAS_ABLATE & 2)) return;
-    const int64_t o = out.start(row);
-    if constexpr (PART || WIDE) {
-        const uint32_t nnz = PART ? (uint32_t)nnz_row : base_rank;
+    if constexpr (WIDE) {
+        const int64_t ow = out.start(row);
+        const uint32_t n = base_rank;
         for (uint32_t s = lane; s < S; s += TEAM) {
             const int32_t cc = t.key[s];
             if (cc != EMPTY_KEY) {
                 const uint32_t r = (uint32_t)(t.meta[s] >> MT::SHIFT);
-                const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - r) : (int64_t)r);
-                // scattered stores: plain (non-temporal partial lines measured 2x slower)
+                const int64_t pos = ow + (out.order == 0 ? (int64_t)(n - 1u - r) : (int64_t)r);
                 out.col[pos] = cc;
                 out.val[pos] = t.val[s];
-                if (out.row_idx) out.row_idx[pos] = (int32_t)row;
             }
         }
     } else {
         // LDS-staged emission: slots -> registers -> (col, val) at their final
         // position in the key/val arrays -> coalesced stores of the row.
         // PER >= ceil(S / TEAM) slots per lane (compile-time, from the kernel).
-        const uint32_t nnz = base_rank;
+        const int64_t ow = out.start(row);
+        const uint32_t n = base_rank;
         int32_t kc[PER];
         uint32_t kr[PER];
         double kv[PER];
@@ -558,16 +607,15 @@ __device__ __forceinline__ void numeric_row(const Rows &A, const Rows &B, int64_
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             if (kc[i] != EMPTY_KEY) {
-                const uint32_t pos = out.order == 0 ? nnz - 1u - kr[i] : kr[i];
+                const uint32_t pos = out.order == 0 ? n - 1u - kr[i] : kr[i];
                 t.key[pos] = kc[i];
                 t.val[pos] = kv[i];
             }
         }
         TM::sync();
-        for (uint32_t e = lane; e < nnz; e += TEAM) {
-            __builtin_nontemporal_store(t.key[e], &out.col[o + e]);
-            __builtin_nontemporal_store(t.val[e], &out.val[o + e]);
-            if (out.row_idx) out.row_idx[o + e] = (int32_t)row;
+        for (uint32_t e = lane; e < n; e += TEAM) {
+            __builtin_nontemporal_store(t.key[e], &out.col[ow + e]);
+            __builtin_nontemporal_store(t.val[e], &out.val[ow + e]);
         }
     }
 }
