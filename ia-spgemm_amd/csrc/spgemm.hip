@@ -820,6 +820,14 @@ ias_plan::~ias_plan() {
         if (b.p) hipFree(b.p);
     for (auto &e : ev)
         if (e) hipEventDestroy(e);
+    for (int i = 0; i < NSIDE; ++i) {
+        if (side[i]) {
+            hipStreamSynchronize((hipStream_t)side[i]);
+            hipStreamDestroy((hipStream_t)side[i]);
+        }
+        if (join_ev[i]) hipEventDestroy(join_ev[i]);
+    }
+    if (fork_ev) hipEventDestroy(fork_ev);
     if (host_counters) hipHostFree(host_counters);
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
 }
@@ -837,7 +845,28 @@ ias_status ias_plan::init(int dev, void *strm) {
         own_stream = true;
     }
     for (auto &e : ev) HIPC(hipEventCreate(&e));
+    for (int i = 0; i < NSIDE; ++i) {
+        hipStream_t t;
+        HIPC(hipStreamCreateWithFlags(&t, hipStreamNonBlocking));
+        side[i] = t;
+        HIPC(hipEventCreateWithFlags(&join_ev[i], hipEventDisableTiming));
+    }
+    HIPC(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     HIPC(hipHostMalloc(&host_counters, 2 * sizeof(Counters)));
+    return IAS_SUCCESS;
+}
+
+ias_status ias_plan::fork() {
+    HIPC(hipEventRecord(fork_ev, (hipStream_t)stream));
+    for (int i = 0; i < NSIDE; ++i) HIPC(hipStreamWaitEvent((hipStream_t)side[i], fork_ev, 0));
+    return IAS_SUCCESS;
+}
+
+ias_status ias_plan::join() {
+    for (int i = 0; i < NSIDE; ++i) {
+        HIPC(hipEventRecord(join_ev[i], (hipStream_t)side[i]));
+        HIPC(hipStreamWaitEvent((hipStream_t)stream, join_ev[i], 0));
+    }
     return IAS_SUCCESS;
 }
 
@@ -917,18 +946,23 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int64_t st[MAX_BINS];
     bin_starts(c1, st);
     int c;
-    for (int b = 1; b <= ss.nval; ++b)
-        if ((c = c1.count[b]) > 0)
-            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(SYM_BINS[b - 1].upper), s, ax, B, SL + st[b]}, nnz);
-    CHECK_LAUNCH("k_symbolic_lds", s);
+    IAS_TRY(fork());
+    int lane_no = 0;
     if ((c = c1.count[sym_part]) > 0) {
-        k_symbolic_part<1024, 4, 14, 256><<<(unsigned)c1.items, 1024, 0, s>>>(
+        hipStream_t t = (hipStream_t)side_stream(lane_no++);
+        k_symbolic_part<1024, 4, 14, 256><<<(unsigned)c1.items, 1024, 0, t>>>(
             ax, B, as<PartItem>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), bm, nnz, &dc2->overflow);
-    CHECK_LAUNCH("k_symbolic_part", s);
-        k_bitmap_prefix<<<c, 256, 0, s>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
-        CHECK_LAUNCH("k_bitmap_prefix", s);
+        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+        CHECK_LAUNCH("k_symbolic_part", t);
     }
+    for (int b = ss.nval; b >= 1; --b)
+        if ((c = c1.count[b]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(SYM_BINS[b - 1].upper), t, ax, B, SL + st[b]}, nnz);
+            CHECK_LAUNCH("k_symbolic_lds", t);
+        }
     HIPC(hipGetLastError());
+    IAS_TRY(join());
 
     // ---- row pointer of C, numeric binning by nnz (and products / nnz)
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
@@ -997,24 +1031,36 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     HIPC(hipEventRecord(ev[3], s));
     int c;
     // big bins first: their long rows start early and the small bins fill in behind
-    if (num_count[part_bin] > 0)
-        k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, s>>>(
+    IAS_TRY(fork());
+    int lane_no = 0;
+    if (num_count[part_bin] > 0) {
+        hipStream_t t = (hipStream_t)side_stream(lane_no++);
+        k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, t>>>(
             ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
-    CHECK_LAUNCH("k_numeric_part", s);
-    if ((c = num_count[wide_bin]) > 0)
-        k_numeric_global<1024, 2, 256><<<c, 1024, 0, s>>>(ax, B, NL + st[wide_bin], as<int64_t>(bufs[B_WSOFF]),
+        CHECK_LAUNCH("k_numeric_part", t);
+    }
+    if ((c = num_count[wide_bin]) > 0) {
+        hipStream_t t = (hipStream_t)side_stream(lane_no++);
+        k_numeric_global<1024, 2, 256><<<c, 1024, 0, t>>>(ax, B, NL + st[wide_bin], as<int64_t>(bufs[B_WSOFF]),
                                                           c, (char *)bufs[B_WS].p, out);
-    CHECK_LAUNCH("k_numeric_global", s);
+        CHECK_LAUNCH("k_numeric_global", t);
+    }
     for (int i = N_DW - 1; i >= 0; --i) {
         const int b = ns.nval + 3 + i;
-        if ((c = num_count[b]) > 0)
-            dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), s, ax, B, NL + st[b]}, out);
-        CHECK_LAUNCH("k_numeric_dw", s);
+        if ((c = num_count[b]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), t, ax, B, NL + st[b]}, out);
+            CHECK_LAUNCH("k_numeric_dw", t);
+        }
     }
     for (int b = ns.nval; b >= 1; --b)
-        if ((c = num_count[b]) > 0)
-            val_bin(VAL_BINS[b - 1].cfg, Launch{c, slots_for(VAL_BINS[b - 1].upper), s, ax, B, NL + st[b]}, out);
-    CHECK_LAUNCH("k_numeric_val", s);
+        if ((c = num_count[b]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            val_bin(VAL_BINS[b - 1].cfg, Launch{c, slots_for(VAL_BINS[b - 1].upper), t, ax, B, NL + st[b]}, out);
+            CHECK_LAUNCH("k_numeric_val", t);
+        }
+    HIPC(hipGetLastError());
+    IAS_TRY(join());
     if (out.row_idx && rows > 0)
         k_fill_rows<<<grid_for(rows * WAVE, 256), 256, 0, s>>>(out.ptr, rows, out.row_idx);
     HIPC(hipGetLastError());

@@ -57,6 +57,16 @@ struct ias_plan {
     bool own_stream = false;
     Buf bufs[B_COUNT];
     hipEvent_t ev[8] = {};
+    // bin kernels run concurrently on side streams forked from / joined to
+    // `stream` (a CU then holds work of several bins at once, and the tail of
+    // one bin overlaps the next)
+    static constexpr int NSIDE = 4;
+    void *side[NSIDE] = {};
+    hipEvent_t fork_ev = nullptr;
+    hipEvent_t join_ev[NSIDE] = {};
+    ias_status fork();
+    ias_status join();
+    void *side_stream(int i) const { return side[i % NSIDE]; }
     void *host_counters = nullptr;
 
     // state carried from symbolic() to numeric()
