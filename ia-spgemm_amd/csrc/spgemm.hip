@@ -21,8 +21,13 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
     return (uint32_t)((key + cap - 1) / cap);
 }
 
-__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod) {
+__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, bool st) {
     if (k <= 0) return 0;
+    if (st) {
+        const int b0 = sp.nval + 3 + sp.ndw;
+        for (int i = 0; i < sp.nst; ++i)
+            if (prod <= sp.upper[b0 + i]) return b0 + i;
+    }
     if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
     const bool val_class =
         sp.ratio_den == 0 || (int64_t)prod * sp.ratio_den > (int64_t)k * sp.ratio_num;
@@ -43,9 +48,10 @@ __device__ __forceinline__ void count_bins(const BinSpec &sp, int b, int32_t k, 
     __syncthreads();
     if (b > 0) {
         atomicAdd(&hist[b], 1);
+        if (sp.ft) atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
+        if (sp.dcap[b] > 0) atomicAdd(&cnt->dup_slots, (unsigned long long)sp.dcap[b]);
         if (b == sp.nval + 1) {
             atomicAdd(&cnt->items, (unsigned long long)nparts_of(k, sp.part_cap));
-            if (sp.ft) atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
         } else if (b == sp.nval + 2) {
             const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
             unsigned long long S = 1;
@@ -109,7 +115,7 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
     const unsigned long long mine = acc[t];
     const int mx0 = (int)min(mine, (unsigned long long)INT32_MAX);
     if (r < rows) prod[r] = mx0;
-    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0) : -1, mx0, cnt);
+    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0, false) : -1, mx0, cnt);
     __shared__ unsigned long long red_sum[AN_BLOCK / WAVE];
     __shared__ int red_max[AN_BLOCK / WAVE];
     unsigned long long sm = (r < rows) ? mine : 0ull;
@@ -138,15 +144,17 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
 constexpr int BIN_BLOCK = 256;
 
 // Counting pass of a binning (numeric and sort binnings; the symbolic one is
-// fused into k_row_products).  prod may be null (class test off).
+// fused into k_row_products).  prod may be null (class test off); a row is
+// streaming-class when stn is given and stn[r] >= 0.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, const int32_t *prod,
-                                                         int64_t rows, BinSpec spec, Counters *cnt) {
+                                                         const int32_t *stn, int64_t rows,
+                                                         BinSpec spec, Counters *cnt) {
     const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + threadIdx.x;
     int b = -1;
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k);
+        b = bin_of(spec, k, prod ? prod[r] : k, stn && stn[r] >= 0);
     }
     count_bins<BIN_BLOCK>(spec, b, k, cnt);
 }
@@ -156,10 +164,12 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
 // partitioned rows get one PartItem per partition (+ a bitmap offset when
 // FT); global-table rows a workspace offset of nextpow2(ceil(k*3/2)) slots.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, const int32_t *prod,
-                                                           int64_t rows, BinSpec spec, Rows A,
-                                                           RowRef *lists, PartItem *items,
-                                                           int64_t *bm_off, int64_t *ws_off,
-                                                           int32_t *nnz_row, Counters *cnt) {
+                                                           const int32_t *stn, int64_t rows,
+                                                           BinSpec spec, Rows A, RowRef *lists,
+                                                           PartItem *items, int64_t *bm_off,
+                                                           int64_t *ws_off, int64_t *dup_off,
+                                                           int32_t *dupn, int32_t *nnz_row,
+                                                           Counters *cnt) {
     __shared__ int hist[MAX_BINS];
     __shared__ int64_t base[MAX_BINS];
     __shared__ int64_t bin_start[MAX_BINS];
@@ -179,8 +189,9 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k);
+        b = bin_of(spec, k, prod ? prod[r] : k, stn && stn[r] >= 0);
         if (b == 0 && spec.zero_nnz) nnz_row[r] = 0;
+        if (b == 0 && dupn) dupn[r] = 0;
         if (b > 0) local = atomicAdd(&hist[b], 1);
     }
     __syncthreads();
@@ -196,12 +207,14 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         ref.row = (int32_t)r;
         ref.n = n;
         lists[bin_start[b] + within] = ref;
+        if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
+        if (spec.dcap[b] > 0) dup_off[r] = (int64_t)atomicAdd(&cnt->dup_cur, (unsigned long long)spec.dcap[b]);
         if (b == part_bin) {
             const uint32_t np = nparts_of(k, spec.part_cap);
             const unsigned long long at = atomicAdd(&cnt->items_cur, (unsigned long long)np);
             for (uint32_t q = 0; q < np; ++q) items[at + q] = PartItem{ref, q, np};
-            if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
             if (spec.zero_nnz) nnz_row[r] = 0;
+            if (dupn) dupn[r] = -1;   // partitioned rows take the table path
         } else if (b == wide_bin) {
             const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
             unsigned long long S = 1;
@@ -222,10 +235,10 @@ template <int SEG, bool NUMERIC>
 __host__ __device__ constexpr size_t team_fixed_bytes() {
     return round16(sizeof(Seg<SEG, NUMERIC>)) + 256;   // segment + 64-int scratch
 }
-// bytes of one team's region: [table | segment | scratch]
+// bytes of one team's region: [table(s) | row arrays | segment | scratch]
 template <int SEG>
-__host__ __device__ constexpr size_t sym_team_bytes(uint32_t S) {
-    return round16(4ull * S) + team_fixed_bytes<SEG, false>();
+__host__ __device__ constexpr size_t sym_team_bytes(uint32_t S, uint32_t W, uint32_t D) {
+    return 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D) + team_fixed_bytes<SEG, false>();
 }
 template <int SEG>
 __host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
@@ -235,27 +248,69 @@ template <int SEG>
 __host__ __device__ constexpr size_t dw_team_bytes(uint32_t S) {
     return 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
 }
+template <int SEG>
+__host__ __device__ constexpr size_t st_team_bytes(uint32_t D) {
+    return round16(8ull * D) + round16(4ull * D) + team_fixed_bytes<SEG, true>();
+}
 
 __device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_t count) {
     if (idx < count) return list[idx];
     return RowRef{0, -1, 0};
 }
 
+// Symbolic pass of the LDS bins: distinct columns (nnz_row), the row's
+// first-touch bitmap with per-word prefix counts, and its duplicate list
+// (dupn[row] = its length, or -1 when it exceeded dcap: the row then takes
+// the table path in the numeric pass).  LDS per team:
+// [keys 4S | minp 4S | bits 4W | dup targets 4D | segment | scratch].
 template <int TEAM, int K, int SEG, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_symbolic_lds(AxView ax, Rows B, const RowRef *list,
-                                                             int32_t count, uint32_t S, int32_t *nnz_row) {
+__global__ __launch_bounds__(TEAM *TPW) void k_symbolic_st(AxView ax, Rows B, const RowRef *list,
+                                                            int32_t count, uint32_t S, uint32_t W,
+                                                            uint32_t D, int32_t *nnz_row, Bitmap bm,
+                                                            const int64_t *dup_off, int32_t *dupn,
+                                                            int32_t *gdupt) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    using TM = Team<TEAM>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    unsigned char *base = smem + (size_t)team * sym_team_bytes<SEG>(S);
+    unsigned char *base = smem + (size_t)team * sym_team_bytes<SEG>(S, W, D);
     int32_t *keys = (int32_t *)base;
-    auto &seg = *(Seg<SEG, false> *)(base + round16(4ull * S));
-    int *scratch = (int *)(base + round16(4ull * S) + round16(sizeof(Seg<SEG, false>)));
+    uint32_t *minp = (uint32_t *)(base + round16(4ull * S));
+    uint32_t *lbits = (uint32_t *)(base + 2 * round16(4ull * S));
+    int32_t *dupt = (int32_t *)(base + 2 * round16(4ull * S) + round16(4ull * W));
+    unsigned char *fixed = base + 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D);
+    auto &seg = *(Seg<SEG, false> *)fixed;
+    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, false>)));
     const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
-    SymTable<false> tb{keys, nullptr, S};
-    const int32_t n = symbolic_row<TEAM, K, SEG, false>(ax, B, ref, tb, 0, 1, seg, scratch, nullptr,
-                                                        nullptr, nullptr);
-    if (ref.row >= 0 && Team<TEAM>::lane() == 0) nnz_row[ref.row] = n;
+    SymTable<true> tb{keys, minp, S};
+    uint32_t ndup = 0, nprod = 0;
+    const int32_t n = symbolic_row_st<TEAM, K, SEG>(ax, B, ref, tb, seg, scratch, lbits, W, dupt, D,
+                                                    ndup, nprod);
+    const int lane = TM::lane();
+    const int64_t row = ref.row;
+    const int64_t off = row >= 0 ? bm.off[row] : 0;
+    // bitmap words and their exclusive prefix popcounts (team-uniform loop)
+    const uint32_t nw = (nprod + 31) / 32;
+    int carry = 0;
+    for (uint32_t w0 = 0; w0 < nw; w0 += TEAM) {
+        const uint32_t w = w0 + lane;
+        const uint32_t word = w < nw ? lbits[w] : 0u;
+        int tot;
+        const int ex = TM::excl_sum(__popc(word), tot, scratch);
+        if (w < nw) {
+            bm.bits[off + w] = word;
+            bm.pref[off + w] = (uint32_t)(carry + ex);
+        }
+        carry += tot;
+    }
+    if (row < 0) return;
+    const bool fits = ndup <= D;
+    if (fits)
+        for (uint32_t i = lane; i < ndup; i += TEAM) gdupt[dup_off[row] + i] = dupt[i];
+    if (lane == 0) {
+        nnz_row[row] = n;
+        dupn[row] = fits ? (int32_t)ndup : -1;
+    }
 }
 
 // One workgroup per (row, hash partition): distinct columns of the partition
@@ -355,6 +410,31 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const 
     NumTable<false> tb{keys, meta, nullptr, 1u << LOG2S};
     numeric_row<TEAM, K, SEG, M_DWPART, 1>(ax, B, it.ref, tb, it.part, it.nparts, bm.bits + bm.off[row],
                                            bm.pref + bm.off[row], seg, scratch, out, overflow);
+}
+
+// Streaming bins (rows whose duplicates fit their list): no hash table;
+// LDS per team [duplicate values 8D | duplicate targets 4D | segment | scratch].
+template <int TEAM, int K, int SEG, int TPW>
+__global__ __launch_bounds__(TEAM *TPW) void k_numeric_st(AxView ax, Rows B, const RowRef *list,
+                                                           int32_t count, uint32_t D, Bitmap bm,
+                                                           const int64_t *dup_off, const int32_t *dupn,
+                                                           const int32_t *gdupt, Out out) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    unsigned char *base = smem + (size_t)team * st_team_bytes<SEG>(D);
+    double *dupval = (double *)base;
+    int32_t *dupt = (int32_t *)(base + round16(8ull * D));
+    unsigned char *fixed = base + round16(8ull * D) + round16(4ull * D);
+    auto &seg = *(Seg<SEG, true> *)fixed;
+    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, true>)));
+    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
+    const int64_t row = ref.row;
+    const int64_t off = row >= 0 ? bm.off[row] : 0;
+    const int32_t nd = row >= 0 ? dupn[row] : 0;
+    const int32_t *gd = row >= 0 ? gdupt + dup_off[row] : gdupt;
+    numeric_row_st<TEAM, K, SEG>(ax, B, ref, bm.bits + off, bm.pref + off, gd, nd, dupval, dupt, seg,
+                                 scratch, out);
 }
 
 template <int TEAM, int K, int SEG>
@@ -634,9 +714,15 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
-static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 3 <= MAX_BINS, "bins");
+static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + N_SYM + 3 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
+static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)((upper + 31) / 32); }
+// duplicate-list capacity of a symbolic bin: rows with more duplicate
+// products than this take the table path in the numeric pass
+static constexpr int32_t dcap_for(int32_t upper) {
+    return upper / 8 < 8 ? 8 : (upper / 8 > 256 ? 256 : upper / 8);
+}
 
 // TEAM * PER of each value configuration in val_bin(): the emission loop
 // visits that many slots, so it must cover every bin's S.
@@ -652,7 +738,10 @@ static BinSpec sym_spec() {
     BinSpec s{};
     s.nval = N_SYM;
     s.ndw = 0;
-    for (int i = 0; i < N_SYM; ++i) s.upper[i + 1] = SYM_BINS[i].upper;
+    for (int i = 0; i < N_SYM; ++i) {
+        s.upper[i + 1] = SYM_BINS[i].upper;
+        s.dcap[i + 1] = dcap_for(SYM_BINS[i].upper);
+    }
     s.ratio_num = 0;
     s.ratio_den = 0;
     s.part_cap = SYM_PART_CAP;
@@ -668,6 +757,9 @@ static BinSpec num_spec() {
     s.ndw = N_DW;
     for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
     for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
+    // streaming rows by products, in the symbolic bins' layout
+    s.nst = N_SYM;
+    for (int i = 0; i < N_SYM; ++i) s.upper[N_VAL + 3 + N_DW + i] = SYM_BINS[i].upper;
     s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
     s.ratio_den = 2;
     s.part_cap = NUM_PART_CAP;
@@ -697,25 +789,57 @@ struct Launch {
     const RowRef *list;
 };
 
+// duplicate lists and bitmap of the streaming path
+struct StArgs {
+    Bitmap bm;
+    int64_t *dup_off;
+    int32_t *dupn;
+    int32_t *dupt;
+};
+
 template <int TEAM, int K, int SEG, int TPW>
-static void sym_launch(const Launch &l, int32_t *nnz) {
-    auto kern = k_symbolic_lds<TEAM, K, SEG, TPW>;
+static void sym_launch(const Launch &l, uint32_t W, uint32_t D, int32_t *nnz, const StArgs &a) {
+    auto kern = k_symbolic_st<TEAM, K, SEG, TPW>;
     static bool done = false;
-    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(l.S);
+    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(l.S, W, D);
     allow_lds(kern, done, lds);
-    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, nnz);
+    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, W, D, nnz, a.bm,
+                                                       a.dup_off, a.dupn, a.dupt);
 }
 
-static void sym_bin(int cfg, const Launch &l, int32_t *nnz) {
+static void sym_bin(int cfg, const Launch &l, uint32_t W, uint32_t D, int32_t *nnz, const StArgs &a) {
     switch (cfg) {
-        case 0: sym_launch<16, 4, 16, 16>(l, nnz); break;
-        case 1: sym_launch<32, 4, 32, 8>(l, nnz); break;
-        case 2: sym_launch<64, 4, 64, 4>(l, nnz); break;
-        case 3: sym_launch<64, 8, 64, 4>(l, nnz); break;
-        case 4: sym_launch<128, 8, 128, 1>(l, nnz); break;
-        case 5: sym_launch<256, 8, 256, 1>(l, nnz); break;
-        case 6: sym_launch<512, 8, 256, 1>(l, nnz); break;
-        default: sym_launch<1024, 4, 256, 1>(l, nnz); break;
+        case 0: sym_launch<16, 4, 16, 16>(l, W, D, nnz, a); break;
+        case 1: sym_launch<32, 4, 32, 8>(l, W, D, nnz, a); break;
+        case 2: sym_launch<64, 4, 64, 4>(l, W, D, nnz, a); break;
+        case 3: sym_launch<64, 8, 64, 4>(l, W, D, nnz, a); break;
+        case 4: sym_launch<128, 8, 128, 1>(l, W, D, nnz, a); break;
+        case 5: sym_launch<256, 8, 256, 1>(l, W, D, nnz, a); break;
+        case 6: sym_launch<512, 8, 256, 1>(l, W, D, nnz, a); break;
+        default: sym_launch<1024, 4, 256, 1>(l, W, D, nnz, a); break;
+    }
+}
+
+template <int TEAM, int K, int SEG, int TPW>
+static void st_launch(const Launch &l, uint32_t D, const StArgs &a, const Out &out) {
+    auto kern = k_numeric_st<TEAM, K, SEG, TPW>;
+    static bool done = false;
+    const size_t lds = (size_t)TPW * st_team_bytes<SEG>(D);
+    allow_lds(kern, done, lds);
+    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, D, a.bm, a.dup_off, a.dupn,
+                                                       a.dupt, out);
+}
+
+static void st_bin(int cfg, const Launch &l, uint32_t D, const StArgs &a, const Out &out) {
+    switch (cfg) {
+        case 0: st_launch<16, 4, 16, 16>(l, D, a, out); break;
+        case 1: st_launch<32, 4, 32, 8>(l, D, a, out); break;
+        case 2: st_launch<64, 4, 64, 4>(l, D, a, out); break;
+        case 3: st_launch<64, 8, 64, 4>(l, D, a, out); break;
+        case 4: st_launch<128, 8, 128, 1>(l, D, a, out); break;
+        case 5: st_launch<256, 8, 256, 1>(l, D, a, out); break;
+        case 6: st_launch<512, 8, 256, 1>(l, D, a, out); break;
+        default: st_launch<1024, 4, 256, 1>(l, D, a, out); break;
     }
 }
 
@@ -894,6 +1018,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_NLIST, sizeof(RowRef) * (rows + 1)));
     IAS_TRY(reserve(B_BMOFF, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(reserve(B_WSOFF, sizeof(int64_t) * (rows + 1)));
+    IAS_TRY(reserve(B_DUPOFF, sizeof(int64_t) * (rows + 1)));
+    IAS_TRY(reserve(B_DUPN, sizeof(int32_t) * (rows + 1)));
     IAS_TRY(reserve(B_CNT, sizeof(Counters)));
     IAS_TRY(reserve(B_CNT2, sizeof(Counters)));
     IAS_TRY(reserve(B_PTR, sizeof(int64_t) * (rows + 1)));
@@ -927,20 +1053,19 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // ---- symbolic binning + symbolic
     IAS_TRY(reserve(B_SITEM, sizeof(PartItem) * (size_t)(c1.items + 1)));
     const int sym_part = ss.nval + 1;
-    Bitmap bm{nullptr, nullptr, as<int64_t>(bufs[B_BMOFF])};
-    if (c1.count[sym_part] > 0) {
-        IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
-        IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
-        bm.bits = as<uint32_t>(bufs[B_BITS]);
-        bm.pref = as<uint32_t>(bufs[B_BPREF]);
-        HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
-    }
+    // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
+    IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
+    IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
+    IAS_TRY(reserve(B_DUPT, sizeof(int32_t) * (c1.dup_slots + 1)));
+    Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
+    const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
+    if (c1.count[sym_part] > 0) HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
     RowRef *SL = as<RowRef>(bufs[B_SLIST]);
     int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
     if (rows > 0)
         k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            as<int32_t>(bufs[B_PROD]), nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
-            as<int64_t>(bufs[B_BMOFF]), nullptr, nnz, dc);
+            as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
+            as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, dc);
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
     HIPC(hipEventRecord(ev[1], s));
     int64_t st[MAX_BINS];
@@ -958,8 +1083,10 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
-            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(SYM_BINS[b - 1].upper), t, ax, B, SL + st[b]}, nnz);
-            CHECK_LAUNCH("k_symbolic_lds", t);
+            const int32_t u = SYM_BINS[b - 1].upper;
+            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(u), t, ax, B, SL + st[b]}, words_for(u),
+                    (uint32_t)dcap_for(u), nnz, sa);
+            CHECK_LAUNCH("k_symbolic_st", t);
         }
     HIPC(hipGetLastError());
     IAS_TRY(join());
@@ -973,11 +1100,11 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART]), nb);
         k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
     CHECK_LAUNCH("scan", s);
-        k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), rows,
-                                                                    ns, dc2);
+        k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
+                                                                    rows, ns, dc2);
         k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
-            nnz, as<int32_t>(bufs[B_PROD]), rows, ns, A, as<RowRef>(bufs[B_NLIST]),
-            as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, dc2);
+            nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
+            as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr, dc2);
     CHECK_LAUNCH("numeric binning", s);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
@@ -1028,6 +1155,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     Counters *dc2 = as<Counters>(bufs[B_CNT2]);
     const AxView ax = ax_view();
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
+    const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
     HIPC(hipEventRecord(ev[3], s));
     int c;
     // big bins first: their long rows start early and the small bins fill in behind
@@ -1051,6 +1179,15 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
             dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), t, ax, B, NL + st[b]}, out);
             CHECK_LAUNCH("k_numeric_dw", t);
+        }
+    }
+    for (int i = N_SYM - 1; i >= 0; --i) {
+        const int b = ns.nval + 3 + N_DW + i;
+        if ((c = num_count[b]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            st_bin(SYM_BINS[i].cfg, Launch{c, 0, t, ax, B, NL + st[b]}, (uint32_t)dcap_for(SYM_BINS[i].upper),
+                   sa, out);
+            CHECK_LAUNCH("k_numeric_st", t);
         }
     }
     for (int b = ns.nval; b >= 1; --b)
@@ -1112,9 +1249,10 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
     // the scatter's row extents are not used by the sort kernels (they read ptr/len)
     const Rows span{ptr, len, stride, nullptr, nullptr};
-    k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, rows, spec, dc);
-    k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, rows, spec, span, lists,
-                                                                  nullptr, nullptr, offs, nullptr, dc);
+    k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
+    k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
+                                                                  lists, nullptr, nullptr, offs, nullptr,
+                                                                  nullptr, nullptr, dc);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));

@@ -8,20 +8,22 @@
 
 namespace ias {
 
-constexpr int MAX_BINS = 36;   // 0 = nothing to do, 1..nval = LDS (value) bins, nval+1 =
+constexpr int MAX_BINS = 48;   // 0 = nothing to do, 1..nval = LDS (value) bins, nval+1 =
                                // hash partitions, nval+2 = global-memory table,
-                               // nval+3.. = direct-write LDS bins
+                               // nval+3.. = direct-write LDS bins, then streaming bins
 
 // How a pass bins its rows by `key` (products or nnz).
 struct BinSpec {
     int32_t nval;              // value bins 1..nval cover key <= upper[nval]
     int32_t ndw;               // direct-write bins nval+3 .. nval+2+ndw
+    int32_t nst;               // streaming bins (by products) after the direct-write bins
     int32_t upper[MAX_BINS];   // per LDS bin, indexed by bin number
     int32_t ratio_num;         // value class iff prod * ratio_den > key * ratio_num
     int32_t ratio_den;         //   (ratio_den == 0: every row is value class)
     int32_t part_cap;          // keys per hash partition in bin nval+1
     int32_t wide_min;          // key >= wide_min -> bin nval+2 (0: never)
-    int32_t ft;                // give partitioned rows a first-touch bitmap
+    int32_t dcap[MAX_BINS];    // duplicate-list capacity per LDS bin (symbolic; 0: none)
+    int32_t ft;                // give every listed row a first-touch bitmap
     int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
 };
 
@@ -31,7 +33,8 @@ struct Counters {
     unsigned long long items;     // (row, partition) work items
     unsigned long long bm_words;  // first-touch bitmap words
     unsigned long long ws_slots;  // global-table slots
-    unsigned long long items_cur, bm_cur, ws_cur;   // scatter-pass cursors
+    unsigned long long dup_slots; // duplicate-list slots
+    unsigned long long items_cur, bm_cur, ws_cur, dup_cur;   // scatter-pass cursors
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
@@ -45,7 +48,7 @@ struct Counters {
 struct ias_plan {
     enum {
         B_AXS, B_AXL, B_AXV, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
-        B_CNT, B_CNT2, B_PTR, B_PART, B_WS,
+        B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
     };
     struct Buf {

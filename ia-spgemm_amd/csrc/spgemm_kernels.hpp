@@ -252,6 +252,22 @@ struct SymTable {
         }
         return -1;
     }
+    // FT tables: slot of c (created when absent), first-touch position kept
+    // as the min product index; -1 when full.
+    __device__ __forceinline__ int insert_slot(int32_t c, uint32_t p, bool &made) const {
+        uint32_t s = slot_hash(c, size);
+        for (uint32_t probe = 0; probe < size; ++probe) {
+            const int32_t prev = atomicCAS(&key[s], EMPTY_KEY, c);
+            if (prev == EMPTY_KEY || prev == c) {
+                atomicMin(&minp[s], p);
+                made = prev == EMPTY_KEY;
+                return (int)s;
+            }
+            s = (s + 1u == size) ? 0u : s + 1u;
+        }
+        made = false;
+        return -1;
+    }
 };
 
 // Numeric table, LDS flavour: meta = rank << 13 | owner (owner 0x1FFF = none,
@@ -409,6 +425,170 @@ __device__ __forceinline__ int32_t symbolic_row(const AxView &ax, const Rows &B,
     }
     if (full) atomicOr(overflow, 1);
     return TM::sum(created, scratch);
+}
+
+// ---------------------------------------------------------------- symbolic, streaming rows
+// Symbolic pass of an LDS-bin row that also prepares the table-free numeric
+// pass (numeric_row_st): keys + first-touch position per distinct column,
+// then
+//   * the row's first-touch bitmap (bit p set iff product p is the first
+//     touch of its column), built in `lbits` (ceil(P/32) words);
+//   * the targets of the row's duplicate products (product index of the
+//     first touch of the same column), in product order, in `dupt`
+//     (at most dcap of them; *ndup = the count, which may exceed dcap).
+// Returns the number of distinct columns.
+template <int TEAM, int K, int SEG>
+__device__ __forceinline__ int32_t symbolic_row_st(const AxView &ax, const Rows &B, const RowRef &ref,
+                                                   const SymTable<true> &table, Seg<SEG, false> &sg,
+                                                   int *scratch, uint32_t *lbits, uint32_t nwords,
+                                                   int32_t *dupt, uint32_t dcap, uint32_t &ndup,
+                                                   uint32_t &nprod) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    const uint32_t S = table.size;
+    for (uint32_t s = lane; s < S; s += TEAM) {
+        table.key[s] = EMPTY_KEY;
+        table.minp[s] = 0xFFFFFFFFu;
+    }
+    for (uint32_t w = lane; w < nwords; w += TEAM) lbits[w] = 0u;
+    TM::sync();
+    const int32_t an = ref.n;
+    int created = 0;
+    uint32_t nd = 0;
+    uint32_t pbase = 0;
+    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
+        int nseg;
+        const int P = load_segment<TEAM, SEG, false>(ax, ref.q0, an, seg0, sg, scratch, nseg);
+        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+            int32_t c[K];
+            int slot[K];
+            bool v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int p = p0 + k * TEAM + lane;
+                v[k] = p < P;
+                if (v[k]) {
+                    const int jj = seg_find(sg.pref, nseg, p);
+                    c[k] = B.col[sg.bstart[jj] + (p - sg.pref[jj])];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                slot[k] = -1;
+                if (v[k]) {
+                    bool made;
+                    slot[k] = table.insert_slot(c[k], pbase + p0 + k * TEAM + lane, made);
+                    created += made ? 1 : 0;
+                }
+            }
+            TM::sync();
+            // a product is a duplicate when its column was touched first by an
+            // earlier product (positions are final once the step has synced)
+            bool dup[K];
+            int32_t tgt[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                tgt[k] = 0;
+                dup[k] = false;
+                if (slot[k] >= 0) {
+                    const uint32_t m = table.minp[slot[k]];
+                    dup[k] = m != pbase + (uint32_t)(p0 + k * TEAM + lane);
+                    tgt[k] = (int32_t)m;
+                }
+            }
+            int r[K];
+            const int total = TM::template excl_count_items<K>(dup, r, scratch);
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (dup[k] && nd + (uint32_t)r[k] < dcap) dupt[nd + r[k]] = tgt[k];
+            nd += (uint32_t)total;
+        }
+        pbase += (uint32_t)P;
+        TM::sync();
+    }
+    for (uint32_t s = lane; s < S; s += TEAM)
+        if (table.key[s] != EMPTY_KEY) {
+            const uint32_t p = table.minp[s];
+            atomicOr(&lbits[p >> 5], 1u << (p & 31));
+        }
+    TM::sync();
+    ndup = nd;
+    nprod = pbase;
+    return TM::sum(created, scratch);
+}
+
+// Table-free numeric pass of a streaming row (symbolic_row_st ran on it and
+// its duplicates fit dcap).  A product whose bitmap bit is set is the first
+// touch of its column: rank = set bits before it, and (col, 0.0 + p) goes
+// straight to its final position.  A duplicate's product is parked in
+// dupval[d] (d = duplicates before it); afterwards every column's duplicates
+// are added to its entry in product order.  Global stores of the team are
+// visible to the team after its barriers (one CU, write-through L1).
+template <int TEAM, int K, int SEG>
+__device__ __forceinline__ void numeric_row_st(const AxView &ax, const Rows &B, const RowRef &ref,
+                                               const uint32_t *bits, const uint32_t *bpref,
+                                               const int32_t *gdupt, int32_t ndup, double *dupval,
+                                               int32_t *dupt, Seg<SEG, true> &sg, int *scratch,
+                                               const Out &out) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    const int64_t row = ref.row;
+    int64_t o = 0;
+    uint32_t nnz = 0;
+    if (row >= 0) {
+        o = out.start(row);
+        nnz = (uint32_t)out.len[row];
+    }
+    for (int32_t i = lane; i < ndup; i += TEAM) dupt[i] = gdupt[i];
+    const int32_t an = ref.n;
+    uint32_t pbase = 0;
+    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
+        int nseg;
+        const int P = load_segment<TEAM, SEG, true>(ax, ref.q0, an, seg0, sg, scratch, nseg);
+        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int pl = p0 + k * TEAM + lane;
+                if (pl < P) {
+                    const int jj = seg_find(sg.pref, nseg, pl);
+                    const int64_t kk = sg.bstart[jj] + (pl - sg.pref[jj]);
+                    const int32_t c = B.col[kk];
+                    const double prod = sg.aval[jj] * B.val[kk];
+                    const uint32_t p = pbase + (uint32_t)pl;
+                    const uint32_t word = bits[p >> 5];
+                    const uint32_t below = word & ((1u << (p & 31)) - 1u);
+                    const uint32_t rk = bpref[p >> 5] + (uint32_t)__popc(below);
+                    if ((word >> (p & 31)) & 1u) {
+                        const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+                        out.col[pos] = c;
+                        out.val[pos] = out.first_assign ? prod : 0.0 + prod;
+                    } else {
+                        dupval[p - rk] = prod;
+                    }
+                }
+            }
+        }
+        pbase += (uint32_t)P;
+        TM::sync();
+    }
+    if (ndup == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    TM::sync();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    // one lane per column with duplicates (its first duplicate), in product order
+    for (int32_t i = lane; i < ndup; i += TEAM) {
+        const int32_t t = dupt[i];
+        bool head = true;
+        for (int32_t j = 0; j < i && head; ++j) head = dupt[j] != t;
+        if (!head) continue;
+        const uint32_t p = (uint32_t)t;
+        const uint32_t rk = bpref[p >> 5] + (uint32_t)__popc(bits[p >> 5] & ((1u << (p & 31)) - 1u));
+        const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+        double v = out.val[pos];
+        for (int32_t j = i; j < ndup; ++j)
+            if (dupt[j] == t) v = v + dupval[j];
+        out.val[pos] = v;
+    }
 }
 
 // ---------------------------------------------------------------- numeric
