@@ -7,6 +7,9 @@
 #include "ias_internal.hpp"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <tuple>
 #include <vector>
 
 namespace ias {
@@ -21,13 +24,11 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
     return (uint32_t)((key + cap - 1) / cap);
 }
 
-__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, bool st) {
+// stv: the row's streaming state (-2: none given; >= 0: a streaming row with
+// stv duplicates -> the fix-up bin when it has any, nothing to do otherwise).
+__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv) {
     if (k <= 0) return 0;
-    if (st) {
-        const int b0 = sp.nval + 3 + sp.ndw;
-        for (int i = 0; i < sp.nst; ++i)
-            if (prod <= sp.upper[b0 + i]) return b0 + i;
-    }
+    if (stv >= 0 && sp.nst > 0) return stv > 0 ? sp.nval + 3 + sp.ndw : 0;
     if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
     const bool val_class =
         sp.ratio_den == 0 || (int64_t)prod * sp.ratio_den > (int64_t)k * sp.ratio_num;
@@ -103,6 +104,7 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
         B.row(j, bs, bn);
         const int64_t q = ea - abase;
         if (q >= 0 && q < a_entries) {
+            ax.row[q] = (int32_t)((int64_t)blockIdx.x * AN_BLOCK + lo);
             ax.bstart[q] = bs;
             ax.blen[q] = bn;
             ax.aval[q] = A.val[ea];
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64
     const unsigned long long mine = acc[t];
     const int mx0 = (int)min(mine, (unsigned long long)INT32_MAX);
     if (r < rows) prod[r] = mx0;
-    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0, false) : -1, mx0, cnt);
+    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0, -2) : -1, mx0, cnt);
     __shared__ unsigned long long red_sum[AN_BLOCK / WAVE];
     __shared__ int red_max[AN_BLOCK / WAVE];
     unsigned long long sm = (r < rows) ? mine : 0ull;
@@ -154,7 +156,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k, stn && stn[r] >= 0);
+        b = bin_of(spec, k, prod ? prod[r] : k, stn ? stn[r] : -2);
     }
     count_bins<BIN_BLOCK>(spec, b, k, cnt);
 }
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
                                                            PartItem *items, int64_t *bm_off,
                                                            int64_t *ws_off, int64_t *dup_off,
                                                            int32_t *dupn, int32_t *nnz_row,
-                                                           Counters *cnt) {
+                                                           const int64_t *qstart, Counters *cnt) {
     __shared__ int hist[MAX_BINS];
     __shared__ int64_t base[MAX_BINS];
     __shared__ int64_t bin_start[MAX_BINS];
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     int32_t k = 0;
     if (r < rows) {
         k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k, stn && stn[r] >= 0);
+        b = bin_of(spec, k, prod ? prod[r] : k, stn ? stn[r] : -2);
         if (b == 0 && spec.zero_nnz) nnz_row[r] = 0;
         if (b == 0 && dupn) dupn[r] = 0;
         if (b > 0) local = atomicAdd(&hist[b], 1);
@@ -200,12 +202,17 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     if (b > 0) {
         const int64_t within = base[b] + local;
         RowRef ref;
-        int64_t s;
-        int32_t n;
-        A.row(r, s, n);
-        ref.q0 = s - A.base();
         ref.row = (int32_t)r;
-        ref.n = n;
+        if (qstart) {   // products of the row in the expansion
+            ref.q0 = qstart[r];
+            ref.n = k;
+        } else {        // entries of the row in the expanded A
+            int64_t s;
+            int32_t n;
+            A.row(r, s, n);
+            ref.q0 = s - A.base();
+            ref.n = n;
+        }
         lists[bin_start[b] + within] = ref;
         if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
         if (spec.dcap[b] > 0) dup_off[r] = (int64_t)atomicAdd(&cnt->dup_cur, (unsigned long long)spec.dcap[b]);
@@ -236,9 +243,8 @@ __host__ __device__ constexpr size_t team_fixed_bytes() {
     return round16(sizeof(Seg<SEG, NUMERIC>)) + 256;   // segment + 64-int scratch
 }
 // bytes of one team's region: [table(s) | row arrays | segment | scratch]
-template <int SEG>
 __host__ __device__ constexpr size_t sym_team_bytes(uint32_t S, uint32_t W, uint32_t D) {
-    return 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D) + team_fixed_bytes<SEG, false>();
+    return 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D) + 256;   // + scratch
 }
 template <int SEG>
 __host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
@@ -247,10 +253,6 @@ __host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
 template <int SEG>
 __host__ __device__ constexpr size_t dw_team_bytes(uint32_t S) {
     return 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
-}
-template <int SEG>
-__host__ __device__ constexpr size_t st_team_bytes(uint32_t D) {
-    return round16(8ull * D) + round16(4ull * D) + team_fixed_bytes<SEG, true>();
 }
 
 __device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_t count) {
@@ -262,66 +264,79 @@ __device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_
 // first-touch bitmap with per-word prefix counts, and its duplicate list
 // (dupn[row] = its length, or -1 when it exceeded dcap: the row then takes
 // the table path in the numeric pass).  LDS per team:
-// [keys 4S | minp 4S | bits 4W | dup targets 4D | segment | scratch].
-template <int TEAM, int K, int SEG, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_symbolic_st(AxView ax, Rows B, const RowRef *list,
-                                                            int32_t count, uint32_t S, uint32_t W,
-                                                            uint32_t D, int32_t *nnz_row, Bitmap bm,
-                                                            const int64_t *dup_off, int32_t *dupn,
-                                                            int32_t *gdupt) {
+// [keys 4S | minp 4S | bits 4W | dup targets 4D | scratch].
+// Teams walk rows idx, idx + nteams, ... (one row each when the grid covers
+// the list); the next row's list entry and first columns are loaded while
+// the current row is hashed.  WPE: minimum waves per SIMD the register
+// allocation must allow (1: none).
+template <int TEAM, int K, int TPW, int WPE>
+__global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_symbolic_st(
+    const int32_t *tcol, const RowRef *list, int32_t count, uint32_t S, uint32_t W, uint32_t D,
+    int32_t *nnz_row, Bitmap bm, const int64_t *dup_off, int32_t *dupn, int32_t *gdupt) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     using TM = Team<TEAM>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    unsigned char *base = smem + (size_t)team * sym_team_bytes<SEG>(S, W, D);
+    unsigned char *base = smem + (size_t)team * sym_team_bytes(S, W, D);
+    const size_t tab = 2 * round16(4ull * S);
     int32_t *keys = (int32_t *)base;
     uint32_t *minp = (uint32_t *)(base + round16(4ull * S));
-    uint32_t *lbits = (uint32_t *)(base + 2 * round16(4ull * S));
-    int32_t *dupt = (int32_t *)(base + 2 * round16(4ull * S) + round16(4ull * W));
-    unsigned char *fixed = base + 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D);
-    auto &seg = *(Seg<SEG, false> *)fixed;
-    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, false>)));
-    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
+    uint32_t *lbits = (uint32_t *)(base + tab);
+    int32_t *dupt = (int32_t *)(base + tab + round16(4ull * W));
+    int *scratch = (int *)(base + tab + round16(4ull * W) + round16(4ull * D));
     SymTable<true> tb{keys, minp, S};
-    uint32_t ndup = 0, nprod = 0;
-    const int32_t n = symbolic_row_st<TEAM, K, SEG>(ax, B, ref, tb, seg, scratch, lbits, W, dupt, D,
-                                                    ndup, nprod);
     const int lane = TM::lane();
-    const int64_t row = ref.row;
-    const int64_t off = row >= 0 ? bm.off[row] : 0;
-    // bitmap words and their exclusive prefix popcounts (team-uniform loop)
-    const uint32_t nw = (nprod + 31) / 32;
-    int carry = 0;
-    for (uint32_t w0 = 0; w0 < nw; w0 += TEAM) {
-        const uint32_t w = w0 + lane;
-        const uint32_t word = w < nw ? lbits[w] : 0u;
-        int tot;
-        const int ex = TM::excl_sum(__popc(word), tot, scratch);
-        if (w < nw) {
-            bm.bits[off + w] = word;
-            bm.pref[off + w] = (uint32_t)(carry + ex);
+    const int64_t nteams = (int64_t)gridDim.x * TPW;
+    int64_t idx = (int64_t)blockIdx.x * TPW + team;
+    RowRef ref = ref_at(list, idx, count);
+    int32_t c[K];
+    load_step<TEAM, K>(tcol, ref, 0, c);
+    while (ref.row >= 0) {
+        Timer tmr;
+        tmr.start();
+        const RowRef next = ref_at(list, idx + nteams, count);
+        uint32_t ndup = 0;
+        const int32_t n = symbolic_row_st<TEAM, K>(tcol, ref, next, c, tb, scratch, lbits, W, dupt, D, ndup,
+                                                   tmr);
+        const int64_t row = ref.row;
+        const int64_t off = bm.off[row];
+        // bitmap words and their exclusive prefix popcounts (team-uniform loop)
+        const uint32_t nw = ((uint32_t)ref.n + 31) / 32;
+        int carry = 0;
+        for (uint32_t w0 = 0; w0 < nw; w0 += TEAM) {
+            const uint32_t w = w0 + lane;
+            const uint32_t word = w < nw ? lbits[w] : 0u;
+            int tot;
+            const int ex = TM::excl_sum(__popc(word), tot, scratch);
+            if (w < nw) {
+                bm.bits[off + w] = word;
+                bm.pref[off + w] = (uint32_t)(carry + ex);
+            }
+            carry += tot;
         }
-        carry += tot;
-    }
-    if (row < 0) return;
-    const bool fits = ndup <= D;
-    if (fits)
-        for (uint32_t i = lane; i < ndup; i += TEAM) gdupt[dup_off[row] + i] = dupt[i];
-    if (lane == 0) {
-        nnz_row[row] = n;
-        dupn[row] = fits ? (int32_t)ndup : -1;
+        tmr.mark(6);
+        const bool fits = ndup <= D;
+        if (fits)
+            for (uint32_t i = lane; i < ndup; i += TEAM) gdupt[dup_off[row] + i] = dupt[i];
+        if (lane == 0) {
+            nnz_row[row] = n;
+            dupn[row] = fits ? (int32_t)ndup : -1;
+        }
+        tmr.mark(7);
+        tmr.flush(ilog2(TEAM), lane == 0);
+        TM::sync();   // lbits / dupt / scratch are reused by the next row
+        ref = next;
+        idx += nteams;
     }
 }
 
 // One workgroup per (row, hash partition): distinct columns of the partition
 // (added to nnz_row) and the first-touch bits of the row's bitmap.
-template <int TEAM, int K, int LOG2S, int SEG>
-__global__ __launch_bounds__(TEAM) void k_symbolic_part(AxView ax, Rows B, const PartItem *items,
-                                                        const int32_t *prod, Bitmap bm,
-                                                        int32_t *nnz_row, int *overflow) {
+template <int TEAM, int K, int LOG2S>
+__global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, const PartItem *items,
+                                                        Bitmap bm, int32_t *nnz_row, int *overflow) {
     __shared__ int32_t keys[1 << LOG2S];
     __shared__ uint32_t minp[1 << LOG2S];
-    __shared__ Seg<SEG, false> seg;
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
     const PartItem it = items[blockIdx.x];
@@ -329,10 +344,10 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(AxView ax, Rows B, const
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
     SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
-    const int32_t n = symbolic_row<TEAM, K, SEG, true>(ax, B, it.ref, tb, it.part, it.nparts, seg,
-                                                       scratch, lbits, gbits, overflow);
+    const int32_t n = symbolic_part_row<TEAM, K>(tcol, it.ref, tb, it.part, it.nparts, scratch, lbits,
+                                                 gbits, overflow);
     // publish this partition's first-touch words (one atomic per non-zero word)
-    const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)prod[row] + 31) / 32);
+    const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)it.ref.n + 31) / 32);
     for (int64_t w = threadIdx.x; w < W; w += TEAM)
         if (lbits[w]) atomicOr(&gbits[w], lbits[w]);
     if (threadIdx.x == 0 && n > 0) atomicAdd(&nnz_row[row], n);
@@ -412,29 +427,122 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const 
                                            bm.pref + bm.off[row], seg, scratch, out, overflow);
 }
 
-// Streaming bins (rows whose duplicates fit their list): no hash table;
-// LDS per team [duplicate values 8D | duplicate targets 4D | segment | scratch].
-template <int TEAM, int K, int SEG, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_numeric_st(AxView ax, Rows B, const RowRef *list,
-                                                           int32_t count, uint32_t D, Bitmap bm,
-                                                           const int64_t *dup_off, const int32_t *dupn,
-                                                           const int32_t *gdupt, Out out) {
-    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    unsigned char *base = smem + (size_t)team * st_team_bytes<SEG>(D);
-    double *dupval = (double *)base;
-    int32_t *dupt = (int32_t *)(base + round16(8ull * D));
-    unsigned char *fixed = base + round16(8ull * D) + round16(4ull * D);
-    auto &seg = *(Seg<SEG, true> *)fixed;
-    int *scratch = (int *)(fixed + round16(sizeof(Seg<SEG, true>)));
-    const RowRef ref = ref_at(list, (int64_t)blockIdx.x * TPW + team, count);
-    const int64_t row = ref.row;
-    const int64_t off = row >= 0 ? bm.off[row] : 0;
-    const int32_t nd = row >= 0 ? dupn[row] : 0;
-    const int32_t *gd = row >= 0 ? gdupt + dup_off[row] : gdupt;
-    numeric_row_st<TEAM, K, SEG>(ax, B, ref, bm.bits + off, bm.pref + off, gd, nd, dupval, dupt, seg,
-                                 scratch, out);
+// Streaming rows, flat over A entries (numeric_flat_chunk): 4 waves per
+// workgroup, each wave a FLAT_CHUNK-entry chunk at a time (grid-stride).
+constexpr int FLAT_BLOCK = 256;
+constexpr int FLAT_K = 4;
+
+__global__ __launch_bounds__(FLAT_BLOCK) void k_numeric_flat(AxView ax, Rows B, FlatArgs fa, Out out) {
+    __shared__ FlatEntry ent[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ int32_t pref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    const int w = threadIdx.x / WAVE;
+    const int64_t nchunks = (fa.n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
+    const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
+    const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
+    for (int64_t ch = wid; ch < nchunks; ch += nw) {
+        numeric_flat_chunk<FLAT_K>(ax, B, fa, out, ch * FLAT_CHUNK, ent[w], pref[w]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// Duplicate fix-up of the streaming rows that have duplicates: one wave per row.
+constexpr int FIX_TPW = 4;
+__global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int32_t count, Bitmap bm,
+                                                        const int64_t *dup_off, const int32_t *dupn,
+                                                        const int32_t *gdupt, const double *gdupval,
+                                                        Out out) {
+    __shared__ int32_t dupt[FIX_TPW][256];
+    const int team = threadIdx.x / WAVE;
+    const int64_t idx = (int64_t)blockIdx.x * FIX_TPW + team;
+    if (idx >= count) return;
+    const int64_t row = list[idx].row;
+    const int32_t nd = dupn[row];
+    if (nd <= 0 || nd > 256) return;
+    const int64_t off = bm.off[row];
+    numeric_fixup_row<WAVE>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
+                            gdupval + dup_off[row], nd, dupt[team], out);
+}
+
+// Row-wise analysis helpers: product offset of every row, and the expansion
+// of every A entry's products into tcol (one wave per FLAT_CHUNK entries,
+// lanes over the chunk's products: coalesced B-row reads, contiguous writes).
+__global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_entries, int64_t *poff) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > rows) return;
+    if (r == rows) {
+        poff[r] = axp[n_entries];
+        return;
+    }
+    int64_t s;
+    int32_t n;
+    A.row(r, s, n);
+    poff[r] = axp[s - A.base()];
+}
+
+__global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t *axp, int64_t n_entries,
+                                                       Rows B, int32_t *tcol) {
+    __shared__ int64_t gs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ int64_t bs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ int32_t pref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    const int w = threadIdx.x / WAVE;
+    const int lane = threadIdx.x & (WAVE - 1);
+    const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
+    const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
+    const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
+    for (int64_t ch = wid; ch < nchunks; ch += nw) {
+        const int64_t q = ch * FLAT_CHUNK + lane;
+        int len = 0;
+        if (q < n_entries) {
+            len = ax.blen[q];
+            gs[w][lane] = axp[q];
+            bs[w][lane] = ax.bstart[q];
+        }
+        int x = len;
+#pragma unroll
+        for (int d = 1; d < WAVE; d <<= 1) {
+            const int t = __shfl_up(x, d);
+            if (lane >= d) x += t;
+        }
+        const int T = __shfl(x, WAVE - 1);
+        pref[w][lane] = x - len;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // loads of step i+1 go out before the stores of step i (vmcnt order)
+        constexpr int EK = 8;
+        int32_t c[EK], cn[EK];
+        int64_t dst[EK], dn[EK];
+        auto load = [&](int t0, int32_t (&cc)[EK], int64_t (&dd)[EK]) {
+#pragma unroll
+            for (int k = 0; k < EK; ++k) {
+                const int t = t0 + k * WAVE + lane;
+                dd[k] = -1;
+                if (t < T) {
+                    const int e = seg_find(pref[w], WAVE, t);
+                    const int j = t - pref[w][e];
+                    cc[k] = B.col[bs[w][e] + j];
+                    dd[k] = gs[w][e] + j;
+                }
+            }
+        };
+        if (T > 0) load(0, c, dst);
+        for (int t0 = 0; t0 < T; t0 += WAVE * EK) {
+            if (t0 + WAVE * EK < T) load(t0 + WAVE * EK, cn, dn);
+#pragma unroll
+            for (int k = 0; k < EK; ++k)
+                if (dst[k] >= 0) tcol[dst[k]] = c[k];
+#pragma unroll
+            for (int k = 0; k < EK; ++k) {
+                c[k] = cn[k];
+                dst[k] = dn[k];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 }
 
 template <int TEAM, int K, int SEG>
@@ -714,7 +822,7 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
-static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + N_SYM + 3 <= MAX_BINS, "bins");
+static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 4 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
 static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)((upper + 31) / 32); }
@@ -757,9 +865,8 @@ static BinSpec num_spec() {
     s.ndw = N_DW;
     for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
     for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
-    // streaming rows by products, in the symbolic bins' layout
-    s.nst = N_SYM;
-    for (int i = 0; i < N_SYM; ++i) s.upper[N_VAL + 3 + N_DW + i] = SYM_BINS[i].upper;
+    // streaming rows: one bin, the rows that need a duplicate fix-up
+    s.nst = 1;
     s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
     s.ratio_den = 2;
     s.part_cap = NUM_PART_CAP;
@@ -780,6 +887,42 @@ static void allow_lds(F kernel, bool &done, size_t bytes) {
     }
 }
 
+// Workgroups of `kernel` resident on the whole device at once (cached per
+// kernel, block size, LDS bytes and device).
+template <typename F>
+static int64_t resident_blocks(F kernel, int threads, size_t lds) {
+    static std::mutex mu;
+    static std::map<std::tuple<const void *, int, size_t, int>, int64_t> cache;
+    int dev = 0;
+    hipGetDevice(&dev);
+    const auto key = std::make_tuple((const void *)kernel, threads, lds, dev);
+    {
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    int per_cu = 0, cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)kernel, threads, lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    (void)hipGetLastError();
+    const int64_t v = (int64_t)per_cu * std::max(cus, 1);
+    std::lock_guard<std::mutex> g(mu);
+    cache[key] = v;
+    return v;
+}
+
+// IAS_SYM_PERSIST=1: symbolic teams persist over their bin (grid = resident
+// workgroups) instead of one team per row.
+static bool sym_persist() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SYM_PERSIST");
+        return e && *e && *e != '0';
+    }();
+    return on;
+}
+
 struct Launch {
     int c;
     uint32_t S;
@@ -797,49 +940,30 @@ struct StArgs {
     int32_t *dupt;
 };
 
-template <int TEAM, int K, int SEG, int TPW>
-static void sym_launch(const Launch &l, uint32_t W, uint32_t D, int32_t *nnz, const StArgs &a) {
-    auto kern = k_symbolic_st<TEAM, K, SEG, TPW>;
+template <int TEAM, int K, int TPW, int WPE>
+static void sym_launch(const Launch &l, const int32_t *tcol, uint32_t W, uint32_t D, int32_t *nnz,
+                       const StArgs &a) {
+    auto kern = k_symbolic_st<TEAM, K, TPW, WPE>;
     static bool done = false;
-    const size_t lds = (size_t)TPW * sym_team_bytes<SEG>(l.S, W, D);
+    const size_t lds = (size_t)TPW * sym_team_bytes(l.S, W, D);
     allow_lds(kern, done, lds);
-    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, l.S, W, D, nnz, a.bm,
-                                                       a.dup_off, a.dupn, a.dupt);
+    int64_t grid = grid_for(l.c, TPW);
+    if (sym_persist()) grid = std::min<int64_t>(grid, resident_blocks(kern, TEAM * TPW, lds));
+    kern<<<(unsigned)grid, TEAM * TPW, lds, l.s>>>(tcol, l.list, l.c, l.S, W, D, nnz, a.bm, a.dup_off,
+                                                   a.dupn, a.dupt);
 }
 
-static void sym_bin(int cfg, const Launch &l, uint32_t W, uint32_t D, int32_t *nnz, const StArgs &a) {
+static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, uint32_t D, int32_t *nnz,
+                    const StArgs &a) {
     switch (cfg) {
-        case 0: sym_launch<16, 4, 16, 16>(l, W, D, nnz, a); break;
-        case 1: sym_launch<32, 4, 32, 8>(l, W, D, nnz, a); break;
-        case 2: sym_launch<64, 4, 64, 4>(l, W, D, nnz, a); break;
-        case 3: sym_launch<64, 8, 64, 4>(l, W, D, nnz, a); break;
-        case 4: sym_launch<128, 8, 128, 1>(l, W, D, nnz, a); break;
-        case 5: sym_launch<256, 8, 256, 1>(l, W, D, nnz, a); break;
-        case 6: sym_launch<512, 8, 256, 1>(l, W, D, nnz, a); break;
-        default: sym_launch<1024, 4, 256, 1>(l, W, D, nnz, a); break;
-    }
-}
-
-template <int TEAM, int K, int SEG, int TPW>
-static void st_launch(const Launch &l, uint32_t D, const StArgs &a, const Out &out) {
-    auto kern = k_numeric_st<TEAM, K, SEG, TPW>;
-    static bool done = false;
-    const size_t lds = (size_t)TPW * st_team_bytes<SEG>(D);
-    allow_lds(kern, done, lds);
-    kern<<<grid_for(l.c, TPW), TEAM * TPW, lds, l.s>>>(l.ax, l.B, l.list, l.c, D, a.bm, a.dup_off, a.dupn,
-                                                       a.dupt, out);
-}
-
-static void st_bin(int cfg, const Launch &l, uint32_t D, const StArgs &a, const Out &out) {
-    switch (cfg) {
-        case 0: st_launch<16, 4, 16, 16>(l, D, a, out); break;
-        case 1: st_launch<32, 4, 32, 8>(l, D, a, out); break;
-        case 2: st_launch<64, 4, 64, 4>(l, D, a, out); break;
-        case 3: st_launch<64, 8, 64, 4>(l, D, a, out); break;
-        case 4: st_launch<128, 8, 128, 1>(l, D, a, out); break;
-        case 5: st_launch<256, 8, 256, 1>(l, D, a, out); break;
-        case 6: st_launch<512, 8, 256, 1>(l, D, a, out); break;
-        default: st_launch<1024, 4, 256, 1>(l, D, a, out); break;
+        case 0: sym_launch<16, 4, 16, 6>(l, tcol, W, D, nnz, a); break;
+        case 1: sym_launch<32, 4, 8, 6>(l, tcol, W, D, nnz, a); break;
+        case 2: sym_launch<64, 4, 4, 6>(l, tcol, W, D, nnz, a); break;
+        case 3: sym_launch<64, 8, 4, 4>(l, tcol, W, D, nnz, a); break;
+        case 4: sym_launch<128, 4, 1, 6>(l, tcol, W, D, nnz, a); break;
+        case 5: sym_launch<256, 4, 1, 1>(l, tcol, W, D, nnz, a); break;
+        case 6: sym_launch<512, 4, 1, 1>(l, tcol, W, D, nnz, a); break;
+        default: sym_launch<1024, 2, 1, 1>(l, tcol, W, D, nnz, a); break;
     }
 }
 
@@ -976,17 +1100,21 @@ ias_status ias_plan::init(int dev, void *strm) {
         HIPC(hipEventCreateWithFlags(&join_ev[i], hipEventDisableTiming));
     }
     HIPC(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    const char *e = getenv("IAS_SERIAL");
+    serial = e && *e && *e != '0';
     HIPC(hipHostMalloc(&host_counters, 2 * sizeof(Counters)));
     return IAS_SUCCESS;
 }
 
 ias_status ias_plan::fork() {
+    if (serial) return IAS_SUCCESS;
     HIPC(hipEventRecord(fork_ev, (hipStream_t)stream));
     for (int i = 0; i < NSIDE; ++i) HIPC(hipStreamWaitEvent((hipStream_t)side[i], fork_ev, 0));
     return IAS_SUCCESS;
 }
 
 ias_status ias_plan::join() {
+    if (serial) return IAS_SUCCESS;
     for (int i = 0; i < NSIDE; ++i) {
         HIPC(hipEventRecord(join_ev[i], (hipStream_t)side[i]));
         HIPC(hipStreamWaitEvent((hipStream_t)stream, join_ev[i], 0));
@@ -1007,11 +1135,17 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
+    n_entries = a_entries;
     const BinSpec ss = sym_spec(), ns = num_spec();
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
     IAS_TRY(reserve(B_AXV, sizeof(double) * ae));
+    IAS_TRY(reserve(B_AXR, sizeof(int32_t) * ae));
+    IAS_TRY(reserve(B_AXP, sizeof(int64_t) * (ae + 1)));
+    IAS_TRY(reserve(B_POFF, sizeof(int64_t) * (rows + 1)));
+    const int64_t nbe = (a_entries + SCAN_TILE - 1) / SCAN_TILE;
+    IAS_TRY(reserve(B_PART2, sizeof(int64_t) * (nbe + 2)));
     IAS_TRY(reserve(B_PROD, sizeof(int32_t) * (rows + 1)));
     IAS_TRY(reserve(B_NNZ, sizeof(int32_t) * (rows + 1)));
     IAS_TRY(reserve(B_SLIST, sizeof(RowRef) * (rows + 1)));
@@ -1030,15 +1164,32 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     Counters *hc = (Counters *)host_counters;
     const AxView ax = ax_view();
 
-    // ---- analysis: products per row, expanded A, symbolic bin counts
+    // ---- analysis: products per row, expanded A (+ product offsets), symbolic bin counts
     HIPC(hipEventRecord(ev[0], s));
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     HIPC(hipMemsetAsync(dc2, 0, sizeof(Counters), s));
+    int32_t *axl = as<int32_t>(bufs[B_AXL]);
+    int32_t *axr = as<int32_t>(bufs[B_AXR]);
+    int64_t *axp = as<int64_t>(bufs[B_AXP]);
+    int64_t *poff = as<int64_t>(bufs[B_POFF]);
+    if (!A.ptr && a_entries > 0) {   // ELL padding entries: no products, any valid row
+        HIPC(hipMemsetAsync(axl, 0, sizeof(int32_t) * a_entries, s));
+        HIPC(hipMemsetAsync(axr, 0, sizeof(int32_t) * a_entries, s));
+    }
     if (rows > 0)
         k_row_products<<<grid_for(rows, AN_BLOCK), AN_BLOCK, 0, s>>>(
-            A, B, rows, AxOut{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), as<double>(bufs[B_AXV])},
+            A, B, rows, AxOut{as<int64_t>(bufs[B_AXS]), axl, as<double>(bufs[B_AXV]), axr},
             a_entries, as<int32_t>(bufs[B_PROD]), ss, dc);
     CHECK_LAUNCH("k_row_products", s);
+    if (a_entries > 0) {
+        k_scan_reduce<<<(unsigned)nbe, SCAN_BLOCK, 0, s>>>(axl, a_entries, as<int64_t>(bufs[B_PART2]), nullptr);
+        k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART2]), nbe);
+        k_scan_apply<<<(unsigned)nbe, SCAN_BLOCK, 0, s>>>(axl, a_entries, as<int64_t>(bufs[B_PART2]), axp);
+    } else {
+        HIPC(hipMemsetAsync(axp, 0, sizeof(int64_t), s));
+    }
+    k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff);
+    CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -1050,6 +1201,16 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     flops = (int64_t)c1.flops;
     max_prod = c1.max_prod;
 
+    // ---- expansion: every row's product columns, contiguous
+    IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(flops, 1)));
+    const int32_t *tcol = as<int32_t>(bufs[B_TCOL]);
+    if (a_entries > 0) {
+        const int64_t nchunks = (a_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
+        const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 4096);
+        k_expand<<<grid, FLAT_BLOCK, 0, s>>>(ax, axp, a_entries, B, as<int32_t>(bufs[B_TCOL]));
+    }
+    CHECK_LAUNCH("k_expand", s);
+
     // ---- symbolic binning + symbolic
     IAS_TRY(reserve(B_SITEM, sizeof(PartItem) * (size_t)(c1.items + 1)));
     const int sym_part = ss.nval + 1;
@@ -1057,6 +1218,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
     IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
     IAS_TRY(reserve(B_DUPT, sizeof(int32_t) * (c1.dup_slots + 1)));
+    IAS_TRY(reserve(B_DUPV, sizeof(double) * (c1.dup_slots + 1)));
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
     if (c1.count[sym_part] > 0) HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
@@ -1065,7 +1227,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if (rows > 0)
         k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
-            as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, dc);
+            as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc);
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
     HIPC(hipEventRecord(ev[1], s));
     int64_t st[MAX_BINS];
@@ -1075,8 +1237,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int lane_no = 0;
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        k_symbolic_part<1024, 4, 14, 256><<<(unsigned)c1.items, 1024, 0, t>>>(
-            ax, B, as<PartItem>(bufs[B_SITEM]), as<int32_t>(bufs[B_PROD]), bm, nnz, &dc2->overflow);
+        k_symbolic_part<1024, 4, 14><<<(unsigned)c1.items, 1024, 0, t>>>(
+            tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, &dc2->overflow);
         k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
@@ -1084,7 +1246,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
             const int32_t u = SYM_BINS[b - 1].upper;
-            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(u), t, ax, B, SL + st[b]}, words_for(u),
+            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(u), t, ax, B, SL + st[b]}, tcol, words_for(u),
                     (uint32_t)dcap_for(u), nnz, sa);
             CHECK_LAUNCH("k_symbolic_st", t);
         }
@@ -1104,7 +1266,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                                                     rows, ns, dc2);
         k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
-            as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr, dc2);
+            as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
+            nullptr, dc2);
     CHECK_LAUNCH("numeric binning", s);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
@@ -1181,13 +1344,21 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             CHECK_LAUNCH("k_numeric_dw", t);
         }
     }
-    for (int i = N_SYM - 1; i >= 0; --i) {
-        const int b = ns.nval + 3 + N_DW + i;
-        if ((c = num_count[b]) > 0) {
-            hipStream_t t = (hipStream_t)side_stream(lane_no++);
-            st_bin(SYM_BINS[i].cfg, Launch{c, 0, t, ax, B, NL + st[b]}, (uint32_t)dcap_for(SYM_BINS[i].upper),
-                   sa, out);
-            CHECK_LAUNCH("k_numeric_st", t);
+    // streaming rows: flat pass, then the duplicate fix-up (same stream, ordered)
+    if (n_entries > 0) {
+        hipStream_t t = (hipStream_t)side_stream(lane_no++);
+        const FlatArgs fa{as<int32_t>(bufs[B_AXR]), as<int64_t>(bufs[B_AXP]), as<int64_t>(bufs[B_POFF]),
+                          n_entries, as<int32_t>(bufs[B_TCOL]), bm, sa.dupn, sa.dup_off,
+                          as<double>(bufs[B_DUPV])};
+        const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
+        const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 2048);
+        k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
+        CHECK_LAUNCH("k_numeric_flat", t);
+        const int fb = ns.nval + 3 + N_DW;
+        if ((c = num_count[fb]) > 0) {
+            k_fixup<<<grid_for(c, FIX_TPW), WAVE * FIX_TPW, 0, t>>>(NL + st[fb], c, bm, sa.dup_off, sa.dupn,
+                                                                   sa.dupt, as<double>(bufs[B_DUPV]), out);
+            CHECK_LAUNCH("k_fixup", t);
         }
     }
     for (int b = ns.nval; b >= 1; --b)
@@ -1252,7 +1423,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
     k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
                                                                   lists, nullptr, nullptr, offs, nullptr,
-                                                                  nullptr, nullptr, dc);
+                                                                  nullptr, nullptr, nullptr, dc);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
@@ -1291,6 +1462,29 @@ ias_status ias::ias_sort_rows_device(ias_plan *plan, const int64_t *ptr, int64_t
 ias_status ias::ias_sort_rows_ell_device(ias_plan *plan, const int32_t *nnz_row, int64_t rows,
                                          int32_t K, int32_t *col, double *val) {
     return sort_rows_impl(plan, nullptr, nnz_row, K, rows, col, val);
+}
+
+// Timing builds only: copy out (and reset) the per-phase cycle sums,
+// TIMING_SLOTS x (TIMING_PHASES + 1) values (last = rows timed).
+extern "C" int ias_debug_timing(unsigned long long *out, int n) {
+#if IAS_TIMING
+    const int total = TIMING_SLOTS * (TIMING_PHASES + 1);
+    if (n < total) return -1;
+    hipDeviceSynchronize();
+    static unsigned long long all[TIMING_REPS * TIMING_SLOTS * (TIMING_PHASES + 1)];
+    if (hipMemcpyFromSymbol(all, HIP_SYMBOL(g_timing), sizeof all) != hipSuccess) return -1;
+    for (int i = 0; i < total; ++i) {
+        out[i] = 0;
+        for (int r = 0; r < TIMING_REPS; ++r) out[i] += all[r * total + i];
+    }
+    static unsigned long long zero[TIMING_REPS * TIMING_SLOTS * (TIMING_PHASES + 1)] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_timing), zero, sizeof zero) != hipSuccess) return -1;
+    return total;
+#else
+    (void)out;
+    (void)n;
+    return 0;
+#endif
 }
 
 ias_status ias::ias_shift_device(int64_t *p, int64_t n, int64_t off, void *stream) {

@@ -47,7 +47,7 @@ struct Counters {
 
 struct ias_plan {
     enum {
-        B_AXS, B_AXL, B_AXV, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
+        B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
     };
@@ -69,11 +69,13 @@ struct ias_plan {
     hipEvent_t join_ev[NSIDE] = {};
     ias_status fork();
     ias_status join();
-    void *side_stream(int i) const { return side[i % NSIDE]; }
+    bool serial = false;   // IAS_SERIAL=1: everything on `stream` (per-kernel profiling)
+    void *side_stream(int i) const { return serial ? stream : side[i % NSIDE]; }
     void *host_counters = nullptr;
 
     // state carried from symbolic() to numeric()
     int64_t n_rows = 0;
+    int64_t n_entries = 0;   // stored entries of A (expanded-A length)
     int64_t nnz_total = 0;
     int64_t flops = 0;
     int32_t max_prod = 0;

@@ -39,6 +39,44 @@ constexpr int32_t EMPTY_KEY = -1;
 #define IAS_ABLATE 0
 #endif
 
+// Timing-only builds (-DIAS_TIMING=1, tools/timing.sh; never shipped): per-
+// phase wall-clock cycles of the row kernels, summed per (kind, log2 TEAM)
+// slot into g_timing and read back by ias_debug_timing().
+#ifndef IAS_TIMING
+#define IAS_TIMING 0
+#endif
+constexpr int TIMING_SLOTS = 32, TIMING_PHASES = 8, TIMING_REPS = 32;
+#if IAS_TIMING
+// replicated per workgroup group so the flush atomics do not contend
+__device__ unsigned long long g_timing[TIMING_REPS * TIMING_SLOTS * (TIMING_PHASES + 1)];
+#endif
+struct Timer {
+#if IAS_TIMING
+    unsigned long long acc[TIMING_PHASES] = {};
+    unsigned long long last = 0;
+    __device__ __forceinline__ void start() { last = wall_clock64(); }
+    __device__ __forceinline__ void mark(int i) {
+        const unsigned long long t = wall_clock64();
+        acc[i] += t - last;
+        last = t;
+    }
+    // sampled: one workgroup in 8 reports
+    __device__ __forceinline__ void flush(int slot, bool leader) {
+        if (!leader || (blockIdx.x & 7) != 0) return;
+        unsigned long long *g =
+            g_timing + ((blockIdx.x >> 3) % TIMING_REPS) * (TIMING_SLOTS * (TIMING_PHASES + 1)) +
+            slot * (TIMING_PHASES + 1);
+        for (int i = 0; i < TIMING_PHASES; ++i) atomicAdd(&g[i], acc[i]);
+        atomicAdd(&g[TIMING_PHASES], 1ull);
+    }
+#else
+    __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(int, bool) {}
+#endif
+};
+__host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+
 // ---------------------------------------------------------------- row views
 // An operand's rows: CSR (ptr != nullptr) or ELL (start = i*stride, len[i]).
 struct Rows {
@@ -73,6 +111,7 @@ struct AxOut {
     int64_t *bstart;
     int32_t *blen;
     double *aval;
+    int32_t *row;
 };
 
 // A row of a bin list: its first expanded-A entry and entry count.
@@ -363,86 +402,67 @@ __device__ __forceinline__ int load_segment(const AxView &ax, int64_t q0, int32_
     return total;
 }
 
+// ---------------------------------------------------------------- expansion
+// The product columns of every row, materialised once in product order:
+// tcol[P_off[row] + p] = column of product p of the row (P_off = exclusive
+// prefix of products per row = axp at the row's first A entry).  The row
+// kernels of the symbolic pass then read a row's products as one contiguous
+// run instead of re-deriving and gathering them.
+
 // ---------------------------------------------------------------- symbolic
-// One team counts the distinct columns of one row (or of one hash partition
-// of it when nparts > 1).  FT: also the first-touch position of every column,
-// published as bits of the row's bitmap.  Returns the team's count; *overflow
-// is set when a partition table filled up.
-template <int TEAM, int K, int SEG, bool FT>
-__device__ __forceinline__ int32_t symbolic_row(const AxView &ax, const Rows &B, const RowRef &ref,
-                                                const SymTable<FT> &table, uint32_t part,
-                                                uint32_t nparts, Seg<SEG, false> &sg,
-                                                int *scratch, uint32_t *lbits, uint32_t *gbits,
-                                                int *overflow) {
-    using TM = Team<TEAM>;
-    const int lane = TM::lane();
-    const uint32_t S = table.size;
-    for (uint32_t s = lane; s < S; s += TEAM) {
-        table.key[s] = EMPTY_KEY;
-        if constexpr (FT) table.minp[s] = 0xFFFFFFFFu;
+// K inserts per lane into a keys + first-touch table with all K CASes in
+// flight at once (a per-item probe loop would serialise K LDS round trips);
+// only collided items probe on.  minp keeps the smallest product per column
+// (atomicMin without return).  slot[k] = the column's slot or -1 (none, or
+// table full: *full set).
+template <int K>
+__device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t S, const int32_t (&c)[K],
+                                         const uint32_t (&p)[K], bool (&use)[K], int (&slot)[K],
+                                         int &created, bool &full) {
+    uint32_t s[K];
+    bool pend[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        pend[k] = use[k];
+        s[k] = pend[k] ? slot_hash(c[k], S) : 0u;
+        slot[k] = -1;
     }
-    TM::sync();
-    const int32_t an = ref.n;
-    int created = 0;
-    bool full = false;
-    uint32_t pbase = 0;
-    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
-        int nseg;
-        const int P = load_segment<TEAM, SEG, false>(ax, ref.q0, an, seg0, sg, scratch, nseg);
-        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
-            int32_t c[K];
-            bool v[K];
+    for (uint32_t probe = 0; probe < S; ++probe) {
+        int32_t v[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int p = p0 + k * TEAM + lane;
-                v[k] = p < P;
-                if (v[k]) {
-                    const int jj = seg_find(sg.pref, nseg, p);
-                    c[k] = B.col[sg.bstart[jj] + (p - sg.pref[jj])];
-                }
-            }
+        for (int k = 0; k < K; ++k)
+            if (pend[k]) v[k] = atomicCAS(&key[s[k]], EMPTY_KEY, c[k]);
+        bool again = false;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (v[k] && (nparts <= 1 || part_of(c[k], nparts) == part)) {
-                    const int r = (IAS_ABLATE & 16) ? (c[k] & 1)
-                                                    : table.insert(c[k], pbase + p0 + k * TEAM + lane);
-                    created += r > 0 ? 1 : 0;
-                    full |= r < 0;
-                }
+        for (int k = 0; k < K; ++k) {
+            if (!pend[k]) continue;
+            if (v[k] == EMPTY_KEY || v[k] == c[k]) {
+                created += v[k] == EMPTY_KEY ? 1 : 0;
+                slot[k] = (int)s[k];
+                pend[k] = false;
+            } else {
+                s[k] = (s[k] + 1u == S) ? 0u : s[k] + 1u;
+                again = true;
             }
         }
-        pbase += (uint32_t)P;
-        TM::sync();
+        if (!again) break;
     }
-    if constexpr (FT) {
-        for (uint32_t s = lane; s < S; s += TEAM)
-            if (table.key[s] != EMPTY_KEY) {
-                const uint32_t p = table.minp[s];
-                if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
-                else atomicOr(&gbits[p >> 5], 1u << (p & 31));
-            }
-        TM::sync();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
+        else if (pend[k]) full = true;
     }
-    if (full) atomicOr(overflow, 1);
-    return TM::sum(created, scratch);
 }
 
-// ---------------------------------------------------------------- symbolic, streaming rows
-// Symbolic pass of an LDS-bin row that also prepares the table-free numeric
-// pass (numeric_row_st): keys + first-touch position per distinct column,
-// then
-//   * the row's first-touch bitmap (bit p set iff product p is the first
-//     touch of its column), built in `lbits` (ceil(P/32) words);
-//   * the targets of the row's duplicate products (product index of the
-//     first touch of the same column), in product order, in `dupt`
-//     (at most dcap of them; *ndup = the count, which may exceed dcap).
-// Returns the number of distinct columns.
-template <int TEAM, int K, int SEG>
-__device__ __forceinline__ int32_t symbolic_row_st(const AxView &ax, const Rows &B, const RowRef &ref,
-                                                   const SymTable<true> &table, Seg<SEG, false> &sg,
-                                                   int *scratch, uint32_t *lbits, uint32_t nwords,
-                                                   int32_t *dupt, uint32_t dcap, uint32_t &ndup,
-                                                   uint32_t &nprod) {
+// One team counts the distinct columns of one hash partition of a row whose
+// products are tcol[ref.q0 .. ref.q0 + ref.n), with the first-touch position
+// of every column published as bits of the row's bitmap.  Returns the team's
+// count; *overflow is set when the table filled up.
+template <int TEAM, int K>
+__device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const RowRef &ref,
+                                                     const SymTable<true> &table, uint32_t part,
+                                                     uint32_t nparts, int *scratch, uint32_t *lbits,
+                                                     uint32_t *gbits, int *overflow) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = table.size;
@@ -450,62 +470,126 @@ __device__ __forceinline__ int32_t symbolic_row_st(const AxView &ax, const Rows 
         table.key[s] = EMPTY_KEY;
         table.minp[s] = 0xFFFFFFFFu;
     }
+    TM::sync();
+    const int32_t P = ref.n;
+    const int32_t *pc = tcol + ref.q0;
+    int created = 0;
+    bool full = false;
+    for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+        int32_t c[K];
+        uint32_t pp[K];
+        bool use[K];
+        int slot[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int p = p0 + k * TEAM + lane;
+            c[k] = p < P ? pc[p] : EMPTY_KEY;
+            pp[k] = (uint32_t)p;
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) use[k] = c[k] != EMPTY_KEY && part_of(c[k], nparts) == part;
+        insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
+    }
+    TM::sync();
+    for (uint32_t s = lane; s < S; s += TEAM)
+        if (table.key[s] != EMPTY_KEY) {
+            const uint32_t p = table.minp[s];
+            if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+            else atomicOr(&gbits[p >> 5], 1u << (p & 31));
+        }
+    TM::sync();
+    if (full) atomicOr(overflow, 1);
+    return TM::sum(created, scratch);
+}
+
+// ---------------------------------------------------------------- symbolic, streaming rows
+// Symbolic pass of an LDS-bin row (products tcol[ref.q0 .. + ref.n)) that
+// also prepares the table-free numeric pass: keys + first-touch position per
+// distinct column, then
+//   * the row's first-touch bitmap (bit p set iff product p is the first
+//     touch of its column), built in `lbits` (ceil(P/32) words);
+//   * the targets of the row's duplicate products (product index of the
+//     first touch of the same column), in product order, in `dupt`
+//     (at most dcap of them; *ndup = the count, which may exceed dcap).
+// `c` holds the row's first step of columns on entry (loaded by the caller,
+// so the loads overlap earlier work); the last step loads the first step of
+// `next` into it.  Returns the number of distinct columns.
+template <int TEAM, int K>
+__device__ __forceinline__ void load_step(const int32_t *tcol, const RowRef &ref, int p0, int32_t (&c)[K]) {
+    const int lane = Team<TEAM>::lane();
+    const int32_t *pc = tcol + ref.q0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int p = p0 + k * TEAM + lane;
+        c[k] = p < ref.n ? pc[p] : EMPTY_KEY;
+    }
+}
+
+template <int TEAM, int K>
+__device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const RowRef &ref,
+                                                   const RowRef &next, int32_t (&c)[K],
+                                                   const SymTable<true> &table, int *scratch,
+                                                   uint32_t *lbits, uint32_t nwords, int32_t *dupt,
+                                                   uint32_t dcap, uint32_t &ndup, Timer &tm) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    const uint32_t S = table.size;
+    const int32_t P = ref.n;
+    constexpr int STEP = TEAM * K;
+    for (uint32_t s = lane; s < S; s += TEAM) {
+        table.key[s] = EMPTY_KEY;
+        table.minp[s] = 0xFFFFFFFFu;
+    }
     for (uint32_t w = lane; w < nwords; w += TEAM) lbits[w] = 0u;
     TM::sync();
-    const int32_t an = ref.n;
+    tm.mark(0);
     int created = 0;
     uint32_t nd = 0;
-    uint32_t pbase = 0;
-    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
-        int nseg;
-        const int P = load_segment<TEAM, SEG, false>(ax, ref.q0, an, seg0, sg, scratch, nseg);
-        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
-            int32_t c[K];
-            int slot[K];
-            bool v[K];
+    bool full = false;
+    for (int p0 = 0; p0 < P; p0 += STEP) {
+#if IAS_TIMING
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // timing builds: load wait = phase 1
+        tm.mark(1);
+#endif
+        uint32_t pp[K];
+        bool use[K];
+        int slot[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int p = p0 + k * TEAM + lane;
-                v[k] = p < P;
-                if (v[k]) {
-                    const int jj = seg_find(sg.pref, nseg, p);
-                    c[k] = B.col[sg.bstart[jj] + (p - sg.pref[jj])];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                slot[k] = -1;
-                if (v[k]) {
-                    bool made;
-                    slot[k] = table.insert_slot(c[k], pbase + p0 + k * TEAM + lane, made);
-                    created += made ? 1 : 0;
-                }
-            }
-            TM::sync();
-            // a product is a duplicate when its column was touched first by an
-            // earlier product (positions are final once the step has synced)
-            bool dup[K];
-            int32_t tgt[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                tgt[k] = 0;
-                dup[k] = false;
-                if (slot[k] >= 0) {
-                    const uint32_t m = table.minp[slot[k]];
-                    dup[k] = m != pbase + (uint32_t)(p0 + k * TEAM + lane);
-                    tgt[k] = (int32_t)m;
-                }
-            }
-            int r[K];
-            const int total = TM::template excl_count_items<K>(dup, r, scratch);
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (dup[k] && nd + (uint32_t)r[k] < dcap) dupt[nd + r[k]] = tgt[k];
-            nd += (uint32_t)total;
+        for (int k = 0; k < K; ++k) {
+            pp[k] = (uint32_t)(p0 + k * TEAM + lane);
+            use[k] = c[k] != EMPTY_KEY;
         }
-        pbase += (uint32_t)P;
+        insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
+        // next step's loads (or the next row's first) overlap this step's
+        // synchronisation and scan
+        if (p0 + STEP < P) load_step<TEAM, K>(tcol, ref, p0 + STEP, c);
+        else load_step<TEAM, K>(tcol, next, 0, c);
+        tm.mark(2);
         TM::sync();
+        tm.mark(3);
+        // a product is a duplicate when its column was touched first by an
+        // earlier product (positions are final once the step has synced)
+        bool dup[K];
+        int32_t tgt[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            tgt[k] = 0;
+            dup[k] = false;
+            if (slot[k] >= 0) {
+                const uint32_t m = table.minp[slot[k]];
+                dup[k] = m != pp[k];
+                tgt[k] = (int32_t)m;
+            }
+        }
+        int r[K];
+        const int total = TM::template excl_count_items<K>(dup, r, scratch);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (dup[k] && nd + (uint32_t)r[k] < dcap) dupt[nd + r[k]] = tgt[k];
+        nd += (uint32_t)total;
+        tm.mark(4);
     }
+    TM::sync();
     for (uint32_t s = lane; s < S; s += TEAM)
         if (table.key[s] != EMPTY_KEY) {
             const uint32_t p = table.minp[s];
@@ -513,69 +597,146 @@ __device__ __forceinline__ int32_t symbolic_row_st(const AxView &ax, const Rows 
         }
     TM::sync();
     ndup = nd;
-    nprod = pbase;
-    return TM::sum(created, scratch);
+    const int32_t n = TM::sum(created, scratch);
+    tm.mark(5);
+    return n;
 }
 
-// Table-free numeric pass of a streaming row (symbolic_row_st ran on it and
-// its duplicates fit dcap).  A product whose bitmap bit is set is the first
-// touch of its column: rank = set bits before it, and (col, 0.0 + p) goes
-// straight to its final position.  A duplicate's product is parked in
-// dupval[d] (d = duplicates before it); afterwards every column's duplicates
-// are added to its entry in product order.  Global stores of the team are
-// visible to the team after its barriers (one CU, write-through L1).
-template <int TEAM, int K, int SEG>
-__device__ __forceinline__ void numeric_row_st(const AxView &ax, const Rows &B, const RowRef &ref,
-                                               const uint32_t *bits, const uint32_t *bpref,
-                                               const int32_t *gdupt, int32_t ndup, double *dupval,
-                                               int32_t *dupt, Seg<SEG, true> &sg, int *scratch,
-                                               const Out &out) {
-    using TM = Team<TEAM>;
-    const int lane = TM::lane();
-    const int64_t row = ref.row;
-    int64_t o = 0;
-    uint32_t nnz = 0;
-    if (row >= 0) {
-        o = out.start(row);
-        nnz = (uint32_t)out.len[row];
+// ---------------------------------------------------------------- numeric, streaming rows
+// Table-free numeric pass of the streaming rows (symbolic_row_st ran on them
+// and their duplicates fit dcap), flat over A entries: a wave takes FLAT_CHUNK
+// consecutive entries and walks their products with its lanes (load-balanced
+// by products, independent of row boundaries).  A product whose bitmap bit is
+// set is the first touch of its column: rank = set bits before it in the
+// row, and (col, 0.0 + p) goes straight to its final position.  A duplicate's
+// product is parked at dupval[dup_off[row] + d] (d = duplicates before it in
+// the row) for the fix-up pass (numeric_fixup_row).
+constexpr int FLAT_CHUNK = 64;
+
+struct FlatArgs {
+    const int32_t *ax_row;     // row of every A entry
+    const int64_t *axp;        // product offset of every A entry (exclusive prefix)
+    const int64_t *poff;       // product offset of every row
+    int64_t n_entries;
+    const int32_t *tcol;       // product columns (expansion)
+    Bitmap bm;
+    const int32_t *dupn;       // per row: duplicates (>= 0) or -1 (table path)
+    const int64_t *dup_off;
+    double *dupval;
+};
+
+struct FlatEntry {
+    int64_t g;        // product offset of the entry
+    int64_t bstart;   // B row start
+    int64_t cbase;    // C position base: order 0 -> start + nnz - 1, order 1 -> start
+    int64_t bmw;      // bitmap word offset of the row
+    int64_t dbase;    // duplicate-value base of the row
+    double aval;
+    int32_t p0;       // row-relative product index of the entry's first product
+    int32_t pad;
+};
+
+template <int K>
+__device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows &B, const FlatArgs &fa,
+                                                   const Out &out, int64_t q0, FlatEntry *ent,
+                                                   int32_t *pref) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int64_t q = q0 + lane;
+    int len = 0;
+    if (q < fa.n_entries) {
+        const int32_t row = fa.ax_row[q];
+        const int32_t dn = fa.dupn[row];
+        if (dn >= 0) {
+            len = ax.blen[q];
+            FlatEntry e;
+            e.g = fa.axp[q];
+            e.bstart = ax.bstart[q];
+            e.aval = ax.aval[q];
+            e.p0 = (int32_t)(e.g - fa.poff[row]);
+            const int64_t st = out.start(row);
+            const int32_t nz = out.len[row];
+            e.cbase = out.order == 0 ? st + nz - 1 : st;
+            e.bmw = fa.bm.off[row];
+            e.dbase = fa.dup_off[row];
+            e.pad = 0;
+            ent[lane] = e;
+        }
     }
-    for (int32_t i = lane; i < ndup; i += TEAM) dupt[i] = gdupt[i];
-    const int32_t an = ref.n;
-    uint32_t pbase = 0;
-    for (int32_t seg0 = 0; seg0 < an; seg0 += SEG) {
-        int nseg;
-        const int P = load_segment<TEAM, SEG, true>(ax, ref.q0, an, seg0, sg, scratch, nseg);
-        for (int p0 = 0; p0 < P; p0 += TEAM * K) {
+    // exclusive prefix of the entries' products over the wave
+    int x = len;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int pl = p0 + k * TEAM + lane;
-                if (pl < P) {
-                    const int jj = seg_find(sg.pref, nseg, pl);
-                    const int64_t kk = sg.bstart[jj] + (pl - sg.pref[jj]);
-                    const int32_t c = B.col[kk];
-                    const double prod = sg.aval[jj] * B.val[kk];
-                    const uint32_t p = pbase + (uint32_t)pl;
-                    const uint32_t word = bits[p >> 5];
-                    const uint32_t below = word & ((1u << (p & 31)) - 1u);
-                    const uint32_t rk = bpref[p >> 5] + (uint32_t)__popc(below);
-                    if ((word >> (p & 31)) & 1u) {
-                        const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
-                        out.col[pos] = c;
-                        out.val[pos] = out.first_assign ? prod : 0.0 + prod;
-                    } else {
-                        dupval[p - rk] = prod;
-                    }
-                }
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const int t = __shfl_up(x, d);
+        if (lane >= d) x += t;
+    }
+    const int T = __shfl(x, WAVE - 1);
+    pref[lane] = x - len;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int sgn = out.order == 0 ? -1 : 1;
+    // Software-pipelined: the loads of step i+1 are issued before the stores
+    // of step i (vmcnt retires loads and stores in issue order, so a load
+    // issued after a store would also wait for that store).
+    struct Step {
+        int32_t c[K];
+        double bv[K];
+        uint32_t word[K], pre[K];
+        int ei[K], j[K];
+    };
+    auto load = [&](int t0, Step &S) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int t = t0 + k * WAVE + lane;
+            S.ei[k] = -1;
+            if (t < T) {
+                const int e = seg_find(pref, WAVE, t);
+                S.ei[k] = e;
+                S.j[k] = t - pref[e];
+                const FlatEntry &E = ent[e];
+                S.c[k] = fa.tcol[E.g + S.j[k]];
+                S.bv[k] = B.val[E.bstart + S.j[k]];
+                const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
+                S.word[k] = fa.bm.bits[E.bmw + (p >> 5)];
+                S.pre[k] = fa.bm.pref[E.bmw + (p >> 5)];
             }
         }
-        pbase += (uint32_t)P;
-        TM::sync();
+    };
+    Step cur, nxt;
+    if (T > 0) load(0, cur);
+    for (int t0 = 0; t0 < T; t0 += WAVE * K) {
+        if (t0 + WAVE * K < T) load(t0 + WAVE * K, nxt);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (cur.ei[k] < 0) continue;
+            const FlatEntry &E = ent[cur.ei[k]];
+            const double prod = E.aval * cur.bv[k];
+            const uint32_t p = (uint32_t)(E.p0 + cur.j[k]);
+            const uint32_t rk = cur.pre[k] + (uint32_t)__popc(cur.word[k] & ((1u << (p & 31)) - 1u));
+            if ((cur.word[k] >> (p & 31)) & 1u) {
+                const int64_t pos = E.cbase + sgn * (int64_t)rk;
+                out.col[pos] = cur.c[k];
+                out.val[pos] = out.first_assign ? prod : 0.0 + prod;
+            } else {
+                fa.dupval[E.dbase + (p - rk)] = prod;
+            }
+        }
+        cur = nxt;
     }
-    if (ndup == 0) return;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+}
+
+// Fix-up of one streaming row with duplicates: each column's duplicate
+// products are added to its entry in product order (one lane per column).
+template <int TEAM>
+__device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *bits, const uint32_t *bpref,
+                                                  const int32_t *gdupt, const double *gdupval,
+                                                  int32_t ndup, int32_t *dupt, const Out &out) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    for (int32_t i = lane; i < ndup; i += TEAM) dupt[i] = gdupt[i];
     TM::sync();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    // one lane per column with duplicates (its first duplicate), in product order
+    const int64_t st = out.start(row);
+    const uint32_t nnz = (uint32_t)out.len[row];
     for (int32_t i = lane; i < ndup; i += TEAM) {
         const int32_t t = dupt[i];
         bool head = true;
@@ -583,10 +744,10 @@ __device__ __forceinline__ void numeric_row_st(const AxView &ax, const Rows &B, 
         if (!head) continue;
         const uint32_t p = (uint32_t)t;
         const uint32_t rk = bpref[p >> 5] + (uint32_t)__popc(bits[p >> 5] & ((1u << (p & 31)) - 1u));
-        const int64_t pos = o + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+        const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
         double v = out.val[pos];
         for (int32_t j = i; j < ndup; ++j)
-            if (dupt[j] == t) v = v + dupval[j];
+            if (dupt[j] == t) v = v + gdupval[j];
         out.val[pos] = v;
     }
 }

@@ -16,5 +16,7 @@ timeout -k 10 120 ./ia-spgemm_amd/bin/spgemm-gpu tests/golden/inputs/dia.mtx --a
 timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err &&
 if [ -n "$PROFILE" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-      python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof.log 2>&1
+      python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof.log 2>&1 &&
+  IAS_SERIAL=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_serial -o run --output-format csv -- \
+      python bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof_serial.log 2>&1
 fi

@@ -14,7 +14,7 @@ src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "ia-spgemm_amd/cs
 pkg = os.path.join(root, "ia-spgemm_amd")
 cmd = ["hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-std=c++17", "-fPIC",
        "-I" + os.path.join(root, "include"), "-I" + os.path.join(pkg, "csrc"), "--cuda-device-only",
-       "-c", src, "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"]
+       "-c", src, "-o", "/tmp/_res.o", "-Rpass-analysis=kernel-resource-usage"] + os.environ.get("RES_FLAGS", "").split()
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():

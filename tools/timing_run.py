@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Run C = A*A with a timing build of libias (tools/timing.sh) and print the
+mean per-row microseconds of each phase of the row kernels.
+
+Phases (spgemm_kernels.hpp, Timer marks):
+  symbolic (k_symbolic_st): 0 table clear, 1 wait for column loads, 2 inserts,
+    3 step/segment syncs, 4 duplicate scan, 5 slot scan+bits, 6 bitmap
+    write, 7 duplicate flush
+  numeric (k_numeric_st): 0 setup, 1 segment load, 2 gather+write,
+    3 segment sync, 4 fix-up barrier, 5 duplicate fix-up
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ia-spgemm_amd"))
+import torch  # noqa: E402,F401  (one HIP runtime: torch's)
+import ias  # noqa: E402
+
+SLOTS, PH = 32, 8
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=20)
+    ap.add_argument("--ef", type=float, default=20)
+    ap.add_argument("--seed", type=int, default=2)
+    a = ap.parse_args()
+    A = ias.gen_rmat(a.scale, a.ef, seed=a.seed)
+    f = ias.lib.ias_debug_timing
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    buf = (C.c_ulonglong * (SLOTS * (PH + 1)))()
+    ias.spgemm(A, device=0)          # warm-up
+    f(buf, len(buf))                 # reset
+    _, rep = ias.spgemm(A, device=0)
+    n = f(buf, len(buf))
+    if n <= 0:
+        print("not a timing build"); return
+    print("report ms: symbolic %.3f numeric %.3f total %.3f" % (rep.ms_symbolic, rep.ms_numeric, rep.ms_total))
+    for slot in range(SLOTS):
+        row = buf[slot * (PH + 1):(slot + 1) * (PH + 1)]
+        cnt = row[PH]
+        if not cnt:
+            continue
+        kind = "symbolic" if slot < 16 else "numeric"
+        team = 1 << (slot % 16)
+        us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
+        print("%-8s TEAM %4d rows %8d  per-row us: %s  sum %.2f" % (
+            kind, team, cnt, " ".join("%6.2f" % u for u in us), sum(us)))
+
+
+if __name__ == "__main__":
+    main()
