@@ -825,7 +825,8 @@ constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
 static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 4 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
-static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)((upper + 31) / 32); }
+// first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
+static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upper + 63) / 64)); }
 // duplicate-list capacity of a symbolic bin: rows with more duplicate
 // products than this take the table path in the numeric pass
 static constexpr int32_t dcap_for(int32_t upper) {

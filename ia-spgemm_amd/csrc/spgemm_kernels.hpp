@@ -410,47 +410,31 @@ __device__ __forceinline__ int load_segment(const AxView &ax, int64_t q0, int32_
 // run instead of re-deriving and gathering them.
 
 // ---------------------------------------------------------------- symbolic
-// K inserts per lane into a keys + first-touch table with all K CASes in
-// flight at once (a per-item probe loop would serialise K LDS round trips);
-// only collided items probe on.  minp keeps the smallest product per column
-// (atomicMin without return).  slot[k] = the column's slot or -1 (none, or
-// table full: *full set).
+// K inserts per lane into a keys + first-touch table, one at a time (an LDS
+// CAS must return before the probe goes on; issuing the K CASes together
+// measured slower: LDS atomic throughput, not latency, bounds this loop).
+// minp keeps the smallest product per column (atomicMin without return).
+// slot[k] = the column's slot or -1 (none, or table full: *full set).
 template <int K>
 __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t S, const int32_t (&c)[K],
                                          const uint32_t (&p)[K], bool (&use)[K], int (&slot)[K],
                                          int &created, bool &full) {
-    uint32_t s[K];
-    bool pend[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        pend[k] = use[k];
-        s[k] = pend[k] ? slot_hash(c[k], S) : 0u;
         slot[k] = -1;
-    }
-    for (uint32_t probe = 0; probe < S; ++probe) {
-        int32_t v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (pend[k]) v[k] = atomicCAS(&key[s[k]], EMPTY_KEY, c[k]);
-        bool again = false;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (!pend[k]) continue;
-            if (v[k] == EMPTY_KEY || v[k] == c[k]) {
-                created += v[k] == EMPTY_KEY ? 1 : 0;
-                slot[k] = (int)s[k];
-                pend[k] = false;
-            } else {
-                s[k] = (s[k] + 1u == S) ? 0u : s[k] + 1u;
-                again = true;
+        if (!use[k]) continue;
+        uint32_t s = slot_hash(c[k], S);
+        for (uint32_t probe = 0; probe < S; ++probe) {
+            const int32_t v = atomicCAS(&key[s], EMPTY_KEY, c[k]);
+            if (v == EMPTY_KEY || v == c[k]) {
+                created += v == EMPTY_KEY ? 1 : 0;
+                atomicMin(&minp[s], p[k]);
+                slot[k] = (int)s;
+                break;
             }
+            s = (s + 1u == S) ? 0u : s + 1u;
         }
-        if (!again) break;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
-        else if (pend[k]) full = true;
+        if (slot[k] < 0) full = true;
     }
 }
 
