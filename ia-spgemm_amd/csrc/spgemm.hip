@@ -154,11 +154,26 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
     const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + threadIdx.x;
     int b = -1;
     int32_t k = 0;
+    unsigned long long sp = 0, sn = 0;
     if (r < rows) {
         k = key[r];
         b = bin_of(spec, k, prod ? prod[r] : k, stn ? stn[r] : -2);
+        if (stn && stn[r] >= 0 && k > 0) {   // a streaming row: its work in the flat pass
+            sp = (unsigned long long)(prod ? prod[r] : k);
+            sn = (unsigned long long)k;
+        }
     }
     count_bins<BIN_BLOCK>(spec, b, k, cnt);
+    if (stn) {
+        for (int d = WAVE / 2; d > 0; d >>= 1) {
+            sp += __shfl_down(sp, d);
+            sn += __shfl_down(sn, d);
+        }
+        if ((threadIdx.x & (WAVE - 1)) == 0 && (sp | sn)) {
+            atomicAdd(&cnt->st_prod, sp);
+            atomicAdd(&cnt->st_nnz, sn);
+        }
+    }
 }
 
 // Scatter pass: every listed row gets a RowRef in its bin's compact list
@@ -1286,6 +1301,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     std::copy(c2.count, c2.count + MAX_BINS, num_count);
     num_items = c2.items;
     num_ws = c2.ws_slots;
+    st_prod = (int64_t)c2.st_prod;
+    st_nnz = (int64_t)c2.st_nnz;
     max_nnz = c2.max_nnz;
     if (rep) {
         float a = 0, b = 0;
@@ -1353,7 +1370,9 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                           as<double>(bufs[B_DUPV])};
         const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
         const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 2048);
+        HIPC(hipEventRecord(ev[5], t));
         k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
+        HIPC(hipEventRecord(ev[6], t));
         CHECK_LAUNCH("k_numeric_flat", t);
         const int fb = ns.nval + 3 + N_DW;
         if ((c = num_count[fb]) > 0) {
@@ -1390,6 +1409,10 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         hipEventElapsedTime(&t, ev[0], ev[4]);
         rep->ms_numeric = a;
         rep->ms_total = t;
+        float f = 0;
+        if (n_entries > 0 && hipEventElapsedTime(&f, ev[5], ev[6]) == hipSuccess) rep->ms_stream = f;
+        rep->stream_products = st_prod;
+        rep->stream_nnz = st_nnz;
     }
     return IAS_SUCCESS;
 }

@@ -34,6 +34,7 @@ struct Counters {
     unsigned long long bm_words;  // first-touch bitmap words
     unsigned long long ws_slots;  // global-table slots
     unsigned long long dup_slots; // duplicate-list slots
+    unsigned long long st_prod, st_nnz;   // products / C entries of the streaming rows
     unsigned long long items_cur, bm_cur, ws_cur, dup_cur;   // scatter-pass cursors
     int32_t max_prod;
     int32_t max_nnz;
@@ -82,6 +83,7 @@ struct ias_plan {
     int32_t max_nnz = 0;
     int32_t num_count[ias::MAX_BINS] = {};
     unsigned long long num_items = 0;
+    int64_t st_prod = 0, st_nnz = 0;
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;

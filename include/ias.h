@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define IAS_ABI_VERSION 1
+#define IAS_ABI_VERSION 2   /* 2: ias_report gained ms_stream, stream_products, stream_nnz */
 
 typedef enum ias_status {
     IAS_SUCCESS = 0,
@@ -134,6 +134,11 @@ typedef struct ias_report {
     int64_t nnz_c;
     int64_t max_row_products;
     int64_t max_row_nnz;
+    /* the step's largest launch, k_numeric_flat (streaming rows: C written
+       without a hash table), timed with events on its own stream */
+    double  ms_stream;
+    int64_t stream_products; /* products it processed */
+    int64_t stream_nnz;      /* entries of C it wrote */
 } ias_report;
 
 typedef struct ias_mtx_info {

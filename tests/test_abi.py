@@ -40,7 +40,7 @@ def test_only_c_symbols_exported():
 
 
 def test_version_and_status_strings():
-    assert ias.lib.ias_abi_version() == 1
+    assert ias.lib.ias_abi_version() == 2
     for s in range(12):
         assert ias.lib.ias_status_string(s)
     assert ias.lib.ias_status_string(99) == b"unknown status"
@@ -52,12 +52,19 @@ def test_opts_default():
     assert o.order == 0 and o.output_memory == -1 and o.device == -1 and not o.plan
 
 
-def test_struct_layouts_match_header():
-    # offsets the header implies on LP64
-    assert C.sizeof(ias.Csr) == 56
-    assert ias.Csr.memory.offset == 48
-    assert C.sizeof(ias.Opts) == 32
-    assert C.sizeof(ias.Report) == 80
+def test_struct_layouts_match_header(tmp_path):
+    # the ctypes mirrors against the C compiler's own layout of include/ias.h
+    src = tmp_path / "layout.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "ias.h"\n'
+        'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(ias_csr), '
+        'offsetof(ias_csr, memory), sizeof(ias_opts), sizeof(ias_report), '
+        'offsetof(ias_report, ms_stream), sizeof(ias_coo), sizeof(ias_ell), sizeof(ias_dia));return 0;}\n')
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    assert got == [C.sizeof(ias.Csr), ias.Csr.memory.offset, C.sizeof(ias.Opts), C.sizeof(ias.Report),
+                   ias.Report.ms_stream.offset, C.sizeof(ias.Coo), C.sizeof(ias.Ell), C.sizeof(ias.Dia)]
 
 
 def test_host_alloc_copy_free():
