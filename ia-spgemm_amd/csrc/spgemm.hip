@@ -164,14 +164,27 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
         }
     }
     count_bins<BIN_BLOCK>(spec, b, k, cnt);
-    if (stn) {
+    if (stn) {   // block sums, one pair of atomics per block
+        __shared__ unsigned long long red[2][BIN_BLOCK / WAVE];
         for (int d = WAVE / 2; d > 0; d >>= 1) {
             sp += __shfl_down(sp, d);
             sn += __shfl_down(sn, d);
         }
-        if ((threadIdx.x & (WAVE - 1)) == 0 && (sp | sn)) {
-            atomicAdd(&cnt->st_prod, sp);
-            atomicAdd(&cnt->st_nnz, sn);
+        if ((threadIdx.x & (WAVE - 1)) == 0) {
+            red[0][threadIdx.x / WAVE] = sp;
+            red[1][threadIdx.x / WAVE] = sn;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long a = 0, c = 0;
+            for (int i = 0; i < BIN_BLOCK / WAVE; ++i) {
+                a += red[0][i];
+                c += red[1][i];
+            }
+            if (a | c) {
+                atomicAdd(&cnt->st_prod, a);
+                atomicAdd(&cnt->st_nnz, c);
+            }
         }
     }
 }
@@ -258,8 +271,9 @@ __host__ __device__ constexpr size_t team_fixed_bytes() {
     return round16(sizeof(Seg<SEG, NUMERIC>)) + 256;   // segment + 64-int scratch
 }
 // bytes of one team's region: [table(s) | row arrays | segment | scratch]
+// [keys | minp | bits | word prefixes | duplicate (product, target) pairs | scratch]
 __host__ __device__ constexpr size_t sym_team_bytes(uint32_t S, uint32_t W, uint32_t D) {
-    return 2 * round16(4ull * S) + round16(4ull * W) + round16(4ull * D) + 256;   // + scratch
+    return 2 * round16(4ull * S) + 2 * round16(4ull * W) + round16(8ull * D) + 256;
 }
 template <int SEG>
 __host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
@@ -297,8 +311,9 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     int32_t *keys = (int32_t *)base;
     uint32_t *minp = (uint32_t *)(base + round16(4ull * S));
     uint32_t *lbits = (uint32_t *)(base + tab);
-    int32_t *dupt = (int32_t *)(base + tab + round16(4ull * W));
-    int *scratch = (int *)(base + tab + round16(4ull * W) + round16(4ull * D));
+    uint32_t *lpref = (uint32_t *)(base + tab + round16(4ull * W));
+    uint2 *dups = (uint2 *)(base + tab + 2 * round16(4ull * W));
+    int *scratch = (int *)(base + tab + 2 * round16(4ull * W) + round16(8ull * D));
     SymTable<true> tb{keys, minp, S};
     const int lane = TM::lane();
     const int64_t nteams = (int64_t)gridDim.x * TPW;
@@ -311,7 +326,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         tmr.start();
         const RowRef next = ref_at(list, idx + nteams, count);
         uint32_t ndup = 0;
-        const int32_t n = symbolic_row_st<TEAM, K>(tcol, ref, next, c, tb, scratch, lbits, W, dupt, D, ndup,
+        const int32_t n = symbolic_row_st<TEAM, K>(tcol, ref, next, c, tb, scratch, lbits, W, dups, D, ndup,
                                                    tmr);
         const int64_t row = ref.row;
         const int64_t off = bm.off[row];
@@ -326,20 +341,29 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             if (w < nw) {
                 bm.bits[off + w] = word;
                 bm.pref[off + w] = (uint32_t)(carry + ex);
+                lpref[w] = (uint32_t)(carry + ex);
             }
             carry += tot;
         }
         tmr.mark(6);
         const bool fits = ndup <= D;
-        if (fits)
-            for (uint32_t i = lane; i < ndup; i += TEAM) gdupt[dup_off[row] + i] = dupt[i];
+        if (fits && ndup > 0) {
+            TM::sync();   // lpref complete
+            // duplicate i of the list lands at its product-order index d = p - rank(p)
+            for (uint32_t i = lane; i < ndup; i += TEAM) {
+                const uint2 e = dups[i];
+                const uint32_t w = e.x >> 5;
+                const uint32_t rk = lpref[w] + (uint32_t)__popc(lbits[w] & ((1u << (e.x & 31)) - 1u));
+                gdupt[dup_off[row] + (e.x - rk)] = (int32_t)e.y;
+            }
+        }
         if (lane == 0) {
             nnz_row[row] = n;
             dupn[row] = fits ? (int32_t)ndup : -1;
         }
         tmr.mark(7);
         tmr.flush(ilog2(TEAM), lane == 0);
-        TM::sync();   // lbits / dupt / scratch are reused by the next row
+        TM::sync();   // lbits / dups / scratch are reused by the next row
         ref = next;
         idx += nteams;
     }

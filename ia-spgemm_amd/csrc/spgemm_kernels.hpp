@@ -509,26 +509,34 @@ __device__ __forceinline__ void load_step(const int32_t *tcol, const RowRef &ref
     }
 }
 
+// Clear n 32-bit words at a 16-byte aligned LDS address with 16-byte stores
+// (the caller's allocation covers n rounded up to 4).
+template <int TEAM>
+__device__ __forceinline__ void lds_fill4(uint32_t *a, uint32_t n, uint32_t v) {
+    uint4 *a4 = (uint4 *)a;
+    const uint4 q = make_uint4(v, v, v, v);
+    for (uint32_t i = Team<TEAM>::lane(); i < (n + 3) / 4; i += TEAM) a4[i] = q;
+}
+
 template <int TEAM, int K>
 __device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const RowRef &ref,
                                                    const RowRef &next, int32_t (&c)[K],
                                                    const SymTable<true> &table, int *scratch,
-                                                   uint32_t *lbits, uint32_t nwords, int32_t *dupt,
+                                                   uint32_t *lbits, uint32_t nwords, uint2 *dups,
                                                    uint32_t dcap, uint32_t &ndup, Timer &tm) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = table.size;
     const int32_t P = ref.n;
     constexpr int STEP = TEAM * K;
-    for (uint32_t s = lane; s < S; s += TEAM) {
-        table.key[s] = EMPTY_KEY;
-        table.minp[s] = 0xFFFFFFFFu;
-    }
-    for (uint32_t w = lane; w < nwords; w += TEAM) lbits[w] = 0u;
+    int *dcount = scratch + 60;   // duplicates seen (scratch[0..16) serves the team scans)
+    lds_fill4<TEAM>((uint32_t *)table.key, S, (uint32_t)EMPTY_KEY);
+    lds_fill4<TEAM>(table.minp, S, 0xFFFFFFFFu);
+    lds_fill4<TEAM>(lbits, nwords, 0u);
+    if (lane == 0) *dcount = 0;
     TM::sync();
     tm.mark(0);
     int created = 0;
-    uint32_t nd = 0;
     bool full = false;
     for (int p0 = 0; p0 < P; p0 += STEP) {
 #if IAS_TIMING
@@ -545,42 +553,43 @@ __device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const Ro
         }
         insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
         // next step's loads (or the next row's first) overlap this step's
-        // synchronisation and scan
+        // barrier and duplicate check
         if (p0 + STEP < P) load_step<TEAM, K>(tcol, ref, p0 + STEP, c);
         else load_step<TEAM, K>(tcol, next, 0, c);
         tm.mark(2);
         TM::sync();
         tm.mark(3);
         // a product is a duplicate when its column was touched first by an
-        // earlier product (positions are final once the step has synced)
-        bool dup[K];
-        int32_t tgt[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            tgt[k] = 0;
-            dup[k] = false;
-            if (slot[k] >= 0) {
-                const uint32_t m = table.minp[slot[k]];
-                dup[k] = m != pp[k];
-                tgt[k] = (int32_t)m;
-            }
-        }
-        int r[K];
-        const int total = TM::template excl_count_items<K>(dup, r, scratch);
+        // earlier product (final once the step's inserts have synced; later
+        // steps only bring larger products, so no second barrier is needed).
+        // Duplicates are listed unordered; their product-order index comes
+        // from the finished bitmap (d = p - rank(p)).
 #pragma unroll
         for (int k = 0; k < K; ++k)
-            if (dup[k] && nd + (uint32_t)r[k] < dcap) dupt[nd + r[k]] = tgt[k];
-        nd += (uint32_t)total;
+            if (slot[k] >= 0) {
+                const uint32_t m = table.minp[slot[k]];
+                if (m != pp[k]) {
+                    const int i = atomicAdd(dcount, 1);
+                    if ((uint32_t)i < dcap) dups[i] = make_uint2(pp[k], m);
+                }
+            }
         tm.mark(4);
     }
     TM::sync();
-    for (uint32_t s = lane; s < S; s += TEAM)
-        if (table.key[s] != EMPTY_KEY) {
-            const uint32_t p = table.minp[s];
-            atomicOr(&lbits[p >> 5], 1u << (p & 31));
+    {   // first-touch bits from the table, 4 slots per lane-read
+        const uint4 *k4 = (const uint4 *)table.key;
+        const uint4 *m4 = (const uint4 *)table.minp;
+        for (uint32_t i = lane; i < (S + 3) / 4; i += TEAM) {
+            const uint4 kk = k4[i];
+            const uint4 mm = m4[i];
+            if ((int32_t)kk.x != EMPTY_KEY) atomicOr(&lbits[mm.x >> 5], 1u << (mm.x & 31));
+            if ((int32_t)kk.y != EMPTY_KEY) atomicOr(&lbits[mm.y >> 5], 1u << (mm.y & 31));
+            if ((int32_t)kk.z != EMPTY_KEY) atomicOr(&lbits[mm.z >> 5], 1u << (mm.z & 31));
+            if ((int32_t)kk.w != EMPTY_KEY) atomicOr(&lbits[mm.w >> 5], 1u << (mm.w & 31));
         }
+    }
     TM::sync();
-    ndup = nd;
+    ndup = (uint32_t)*dcount;
     const int32_t n = TM::sum(created, scratch);
     tm.mark(5);
     return n;
