@@ -520,23 +520,38 @@ __global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_e
     poff[r] = axp[s - A.base()];
 }
 
+// Product -> entry mapping without a per-product search: the wave's chunk of
+// entries is compacted to its non-empty entries; for a segment of MW windows
+// of 64 consecutive products, every entry sets the bit of its first product
+// in its window's 64-bit mask (one LDS atomicOr per entry); lane l of a
+// window then belongs to entry ecur + popcount(mask & bits 0..l), and ecur
+// advances by popcount(mask) per window.
+constexpr int FLAT_MW = 64;
+
 __global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t *axp, int64_t n_entries,
                                                        Rows B, int32_t *tcol) {
-    __shared__ int64_t gs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ int64_t bs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ int32_t pref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ int64_t cbs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ int32_t cpref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ unsigned long long masks[FLAT_BLOCK / WAVE][FLAT_MW];
     const int w = threadIdx.x / WAVE;
     const int lane = threadIdx.x & (WAVE - 1);
+    const uint64_t upto = (2ull << lane) - 1ull;   // bits 0..lane
     const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
     const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
     const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     for (int64_t ch = wid; ch < nchunks; ch += nw) {
         const int64_t q = ch * FLAT_CHUNK + lane;
         int len = 0;
+        int64_t g = 0, bsq = 0;
         if (q < n_entries) {
             len = ax.blen[q];
-            gs[w][lane] = axp[q];
-            bs[w][lane] = ax.bstart[q];
+            g = axp[q];
+            bsq = ax.bstart[q];
         }
         int x = len;
 #pragma unroll
@@ -545,42 +560,56 @@ __global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t 
             if (lane >= d) x += t;
         }
         const int T = __shfl(x, WAVE - 1);
-        pref[w][lane] = x - len;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // loads of step i+1 go out before the stores of step i (vmcnt order)
-        constexpr int EK = 8;
-        int32_t c[EK], cn[EK];
-        int64_t dst[EK], dn[EK];
-        auto load = [&](int t0, int32_t (&cc)[EK], int64_t (&dd)[EK]) {
+        const int start = x - len;   // chunk-relative first product
+        const int64_t G0 = __shfl(g, 0) ;   // products of the chunk are tcol[G0 .. G0 + T)
+        const uint64_t nz = __ballot(len > 0);
+        if (len > 0) {
+            const int ci = __popcll(nz & ((1ull << lane) - 1ull));
+            cbs[w][ci] = bsq;
+            cpref[w][ci] = start;
+        }
+        for (int seg0 = 0; seg0 < T; seg0 += WAVE * FLAT_MW) {
+            masks[w][lane] = 0ull;   // FLAT_MW == WAVE
+            wave_sync();
+            if (len > 0 && start >= seg0 && start < seg0 + WAVE * FLAT_MW)
+                atomicOr(&masks[w][(start - seg0) >> 6], 1ull << ((start - seg0) & 63));
+            int ecur = __popcll(__ballot(len > 0 && start < seg0)) - 1;
+            wave_sync();
+            const int nwin = min(FLAT_MW, (T - seg0 + WAVE - 1) / WAVE);
+            // loads of window group i+1 go out before the stores of group i (vmcnt order)
+            constexpr int EK = 8;
+            int32_t c[EK], cn[EK];
+            int tt[EK], tn[EK];
+            auto load = [&](int w0, int32_t (&cc)[EK], int (&ti)[EK]) {
 #pragma unroll
-            for (int k = 0; k < EK; ++k) {
-                const int t = t0 + k * WAVE + lane;
-                dd[k] = -1;
-                if (t < T) {
-                    const int e = seg_find(pref[w], WAVE, t);
-                    const int j = t - pref[w][e];
-                    cc[k] = B.col[bs[w][e] + j];
-                    dd[k] = gs[w][e] + j;
+                for (int k = 0; k < EK; ++k) {
+                    ti[k] = -1;
+                    if (w0 + k < nwin) {
+                        const uint64_t m = masks[w][w0 + k];
+                        const int e = ecur + __popcll(m & upto);
+                        ecur += __popcll(m);
+                        const int t = seg0 + (w0 + k) * WAVE + lane;
+                        if (t < T) {
+                            cc[k] = B.col[cbs[w][e] + (t - cpref[w][e])];
+                            ti[k] = t;
+                        }
+                    }
+                }
+            };
+            load(0, c, tt);
+            for (int w0 = 0; w0 < nwin; w0 += EK) {
+                if (w0 + EK < nwin) load(w0 + EK, cn, tn);
+#pragma unroll
+                for (int k = 0; k < EK; ++k)
+                    if (tt[k] >= 0) tcol[G0 + tt[k]] = c[k];
+#pragma unroll
+                for (int k = 0; k < EK; ++k) {
+                    c[k] = cn[k];
+                    tt[k] = tn[k];
                 }
             }
-        };
-        if (T > 0) load(0, c, dst);
-        for (int t0 = 0; t0 < T; t0 += WAVE * EK) {
-            if (t0 + WAVE * EK < T) load(t0 + WAVE * EK, cn, dn);
-#pragma unroll
-            for (int k = 0; k < EK; ++k)
-                if (dst[k] >= 0) tcol[dst[k]] = c[k];
-#pragma unroll
-            for (int k = 0; k < EK; ++k) {
-                c[k] = cn[k];
-                dst[k] = dn[k];
-            }
+            wave_sync();
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
