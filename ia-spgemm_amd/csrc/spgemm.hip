@@ -469,17 +469,22 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const 
 // Streaming rows, flat over A entries (numeric_flat_chunk): 4 waves per
 // workgroup, each wave a FLAT_CHUNK-entry chunk at a time (grid-stride).
 constexpr int FLAT_BLOCK = 256;
-constexpr int FLAT_K = 4;
+#ifndef FLAT_K
+#define FLAT_K 4
+#endif
+#ifndef FLAT_WPE
+#define FLAT_WPE 4
+#endif
 
-__global__ __launch_bounds__(FLAT_BLOCK) void k_numeric_flat(AxView ax, Rows B, FlatArgs fa, Out out) {
+__global__ __launch_bounds__(FLAT_BLOCK) __attribute__((amdgpu_waves_per_eu(FLAT_WPE))) void k_numeric_flat(AxView ax, Rows B, FlatArgs fa, Out out) {
     __shared__ FlatEntry ent[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ int32_t pref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
+    __shared__ unsigned long long masks[FLAT_BLOCK / WAVE][FLAT_MW];
     const int w = threadIdx.x / WAVE;
     const int64_t nchunks = (fa.n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
     const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
     const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
     for (int64_t ch = wid; ch < nchunks; ch += nw) {
-        numeric_flat_chunk<FLAT_K>(ax, B, fa, out, ch * FLAT_CHUNK, ent[w], pref[w]);
+        numeric_flat_chunk<FLAT_K>(ax, B, fa, out, ch * FLAT_CHUNK, ent[w], masks[w]);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -526,8 +531,6 @@ __global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_e
 // in its window's 64-bit mask (one LDS atomicOr per entry); lane l of a
 // window then belongs to entry ecur + popcount(mask & bits 0..l), and ecur
 // advances by popcount(mask) per window.
-constexpr int FLAT_MW = 64;
-
 __global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t *axp, int64_t n_entries,
                                                        Rows B, int32_t *tcol) {
     __shared__ int64_t cbs[FLAT_BLOCK / WAVE][FLAT_CHUNK];

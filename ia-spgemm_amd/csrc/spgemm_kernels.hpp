@@ -604,7 +604,7 @@ __device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const Ro
 // row, and (col, 0.0 + p) goes straight to its final position.  A duplicate's
 // product is parked at dupval[dup_off[row] + d] (d = duplicates before it in
 // the row) for the fix-up pass (numeric_fixup_row).
-constexpr int FLAT_CHUNK = 64;
+constexpr int FLAT_CHUNK = 64;   // entries per wave chunk (== WAVE)
 
 struct FlatArgs {
     const int32_t *ax_row;     // row of every A entry
@@ -626,22 +626,34 @@ struct FlatEntry {
     int64_t dbase;    // duplicate-value base of the row
     double aval;
     int32_t p0;       // row-relative product index of the entry's first product
-    int32_t pad;
+    int32_t start;    // chunk-relative index of the entry's first product
 };
+
+// Products of the chunk are mapped to their entries by per-window start
+// masks (see k_expand): the chunk's non-empty entries are compacted into
+// `ent`, each sets the bit of its first product in `masks`, and lane l of a
+// 64-product window belongs to entry ecur + popcount(mask & bits 0..l).
+constexpr int FLAT_MW = 64;
 
 template <int K>
 __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows &B, const FlatArgs &fa,
                                                    const Out &out, int64_t q0, FlatEntry *ent,
-                                                   int32_t *pref) {
+                                                   unsigned long long *masks) {
     const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const uint64_t upto = (2ull << lane) - 1ull;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     const int64_t q = q0 + lane;
     int len = 0;
+    FlatEntry e{};
     if (q < fa.n_entries) {
         const int32_t row = fa.ax_row[q];
         const int32_t dn = fa.dupn[row];
         if (dn >= 0) {
             len = ax.blen[q];
-            FlatEntry e;
             e.g = fa.axp[q];
             e.bstart = ax.bstart[q];
             e.aval = ax.aval[q];
@@ -651,8 +663,6 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
             e.cbase = out.order == 0 ? st + nz - 1 : st;
             e.bmw = fa.bm.off[row];
             e.dbase = fa.dup_off[row];
-            e.pad = 0;
-            ent[lane] = e;
         }
     }
     // exclusive prefix of the entries' products over the wave
@@ -663,58 +673,74 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
         if (lane >= d) x += t;
     }
     const int T = __shfl(x, WAVE - 1);
-    pref[lane] = x - len;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int start = x - len;
+    const uint64_t nzb = __ballot(len > 0);
+    if (len > 0) {
+        e.start = start;
+        ent[__popcll(nzb & ((1ull << lane) - 1ull))] = e;
+    }
     const int sgn = out.order == 0 ? -1 : 1;
-    // Software-pipelined: the loads of step i+1 are issued before the stores
-    // of step i (vmcnt retires loads and stores in issue order, so a load
-    // issued after a store would also wait for that store).
     struct Step {
         int32_t c[K];
         double bv[K];
         uint32_t word[K], pre[K];
         int ei[K], j[K];
     };
-    auto load = [&](int t0, Step &S) {
+    for (int seg0 = 0; seg0 < T; seg0 += WAVE * FLAT_MW) {
+        masks[lane] = 0ull;   // FLAT_MW == WAVE
+        wave_sync();
+        if (len > 0 && start >= seg0 && start < seg0 + WAVE * FLAT_MW)
+            atomicOr(&masks[(start - seg0) >> 6], 1ull << ((start - seg0) & 63));
+        int ecur = __popcll(__ballot(len > 0 && start < seg0)) - 1;
+        wave_sync();
+        const int nwin = min(FLAT_MW, (T - seg0 + WAVE - 1) / WAVE);
+        // Software-pipelined: the loads of window group i+1 are issued before
+        // the stores of group i (vmcnt retires loads and stores in issue
+        // order, so a load issued after a store would also wait for it).
+        auto load = [&](int w0, Step &S) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int t = t0 + k * WAVE + lane;
-            S.ei[k] = -1;
-            if (t < T) {
-                const int e = seg_find(pref, WAVE, t);
-                S.ei[k] = e;
-                S.j[k] = t - pref[e];
-                const FlatEntry &E = ent[e];
-                S.c[k] = fa.tcol[E.g + S.j[k]];
-                S.bv[k] = B.val[E.bstart + S.j[k]];
-                const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
-                S.word[k] = fa.bm.bits[E.bmw + (p >> 5)];
-                S.pre[k] = fa.bm.pref[E.bmw + (p >> 5)];
+            for (int k = 0; k < K; ++k) {
+                S.ei[k] = -1;
+                if (w0 + k < nwin) {
+                    const uint64_t m = masks[w0 + k];
+                    const int ei = ecur + __popcll(m & upto);
+                    ecur += __popcll(m);
+                    const int t = seg0 + (w0 + k) * WAVE + lane;
+                    if (t < T) {
+                        const FlatEntry &E = ent[ei];
+                        S.ei[k] = ei;
+                        S.j[k] = t - E.start;
+                        S.c[k] = fa.tcol[E.g + S.j[k]];
+                        S.bv[k] = B.val[E.bstart + S.j[k]];
+                        const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
+                        S.word[k] = fa.bm.bits[E.bmw + (p >> 5)];
+                        S.pre[k] = fa.bm.pref[E.bmw + (p >> 5)];
+                    }
+                }
             }
-        }
-    };
-    Step cur, nxt;
-    if (T > 0) load(0, cur);
-    for (int t0 = 0; t0 < T; t0 += WAVE * K) {
-        if (t0 + WAVE * K < T) load(t0 + WAVE * K, nxt);
+        };
+        Step cur, nxt;
+        load(0, cur);
+        for (int w0 = 0; w0 < nwin; w0 += K) {
+            if (w0 + K < nwin) load(w0 + K, nxt);
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (cur.ei[k] < 0) continue;
-            const FlatEntry &E = ent[cur.ei[k]];
-            const double prod = E.aval * cur.bv[k];
-            const uint32_t p = (uint32_t)(E.p0 + cur.j[k]);
-            const uint32_t rk = cur.pre[k] + (uint32_t)__popc(cur.word[k] & ((1u << (p & 31)) - 1u));
-            if ((cur.word[k] >> (p & 31)) & 1u) {
-                const int64_t pos = E.cbase + sgn * (int64_t)rk;
-                out.col[pos] = cur.c[k];
-                out.val[pos] = out.first_assign ? prod : 0.0 + prod;
-            } else {
-                fa.dupval[E.dbase + (p - rk)] = prod;
+            for (int k = 0; k < K; ++k) {
+                if (cur.ei[k] < 0) continue;
+                const FlatEntry &E = ent[cur.ei[k]];
+                const double prod = E.aval * cur.bv[k];
+                const uint32_t p = (uint32_t)(E.p0 + cur.j[k]);
+                const uint32_t rk = cur.pre[k] + (uint32_t)__popc(cur.word[k] & ((1u << (p & 31)) - 1u));
+                if ((cur.word[k] >> (p & 31)) & 1u) {
+                    const int64_t pos = E.cbase + sgn * (int64_t)rk;
+                    out.col[pos] = cur.c[k];
+                    out.val[pos] = out.first_assign ? prod : 0.0 + prod;
+                } else {
+                    fa.dupval[E.dbase + (p - rk)] = prod;
+                }
             }
+            cur = nxt;
         }
-        cur = nxt;
+        wave_sync();
     }
 }
 
