@@ -410,15 +410,54 @@ __device__ __forceinline__ int load_segment(const AxView &ax, int64_t q0, int32_
 // run instead of re-deriving and gathering them.
 
 // ---------------------------------------------------------------- symbolic
-// K inserts per lane into a keys + first-touch table, one at a time (an LDS
-// CAS must return before the probe goes on; issuing the K CASes together
-// measured slower: LDS atomic throughput, not latency, bounds this loop).
-// minp keeps the smallest product per column (atomicMin without return).
+// K inserts per lane into a keys + first-touch table, one CAS round trip at a
+// time (default).  INSERT_VEC=1 issues the K first-probe CASes back to back
+// (idle items CAS EMPTY over EMPTY at a lane-spread slot: a no-op) and lets
+// only collided items probe on; on MI355X it measured slower (K3' symbolic
+// 8.7 vs 7.6 ms; 12.9 ms when idle items all hit one slot): several
+// returning LDS atomics in flight per wave cost more than they hide.  minp
+// keeps the smallest product per column (atomicMin without return).
 // slot[k] = the column's slot or -1 (none, or table full: *full set).
+#ifndef INSERT_VEC
+#define INSERT_VEC 0
+#endif
 template <int K>
 __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t S, const int32_t (&c)[K],
                                          const uint32_t (&p)[K], bool (&use)[K], int (&slot)[K],
                                          int &created, bool &full) {
+#if INSERT_VEC
+    // round 1: every item's home slot, K CASes back to back (an idle item
+    // CASes EMPTY over EMPTY at its own lane's slot: a no-op, no hot spot)
+    uint32_t s[K];
+    int32_t v[K];
+    const uint32_t idle = (uint32_t)(threadIdx.x % S);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        s[k] = use[k] ? slot_hash(c[k], S) : idle;
+        v[k] = atomicCAS(&key[s[k]], EMPTY_KEY, use[k] ? c[k] : EMPTY_KEY);
+    }
+    // collided items probe on one at a time
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        slot[k] = -1;
+        if (!use[k]) continue;
+        uint32_t t = s[k];
+        int32_t w = v[k];
+        for (uint32_t probe = 1; probe <= S; ++probe) {
+            if (w == EMPTY_KEY || w == c[k]) {
+                created += w == EMPTY_KEY ? 1 : 0;
+                slot[k] = (int)t;
+                break;
+            }
+            t = (t + 1u == S) ? 0u : t + 1u;
+            w = atomicCAS(&key[t], EMPTY_KEY, c[k]);
+        }
+        if (slot[k] < 0) full = true;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
+#else
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         slot[k] = -1;
@@ -436,6 +475,7 @@ __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t 
         }
         if (slot[k] < 0) full = true;
     }
+#endif
 }
 
 // One team counts the distinct columns of one hash partition of a row whose
