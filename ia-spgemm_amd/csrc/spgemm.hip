@@ -28,7 +28,10 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
 // stv duplicates -> the fix-up bin when it has any, nothing to do otherwise).
 __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv) {
     if (k <= 0) return 0;
-    if (stv >= 0 && sp.nst > 0) return stv > 0 ? sp.nval + 3 + sp.ndw : 0;
+    if (stv >= 0 && sp.nst > 0) {   // fix-up bins: short lists (one wave), long lists (sorted)
+        if (stv == 0) return 0;
+        return sp.nval + 3 + sp.ndw + (stv > 256 ? 1 : 0);
+    }
     if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
     const bool val_class =
         sp.ratio_den == 0 || (int64_t)prod * sp.ratio_den > (int64_t)k * sp.ratio_num;
@@ -38,6 +41,12 @@ __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod
     for (int i = 0; i < sp.ndw; ++i)
         if (k <= sp.upper[sp.nval + 3 + i]) return sp.nval + 3 + i;
     return sp.nval + 1;
+}
+
+// duplicate-list capacity of a row in bin b with key k
+__device__ __forceinline__ int32_t dcap_of(const BinSpec &sp, int b, int32_t k) {
+    if (b == sp.nval + 1 && sp.part_dcap_div > 0) return min(k / sp.part_dcap_div, sp.part_dcap_max);
+    return sp.dcap[b];
 }
 
 // Block-level count of rows per bin (+ partition items, bitmap words and
@@ -50,7 +59,8 @@ __device__ __forceinline__ void count_bins(const BinSpec &sp, int b, int32_t k, 
     if (b > 0) {
         atomicAdd(&hist[b], 1);
         if (sp.ft) atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
-        if (sp.dcap[b] > 0) atomicAdd(&cnt->dup_slots, (unsigned long long)sp.dcap[b]);
+        const int32_t dc = dcap_of(sp, b, k);
+        if (dc > 0) atomicAdd(&cnt->dup_slots, (unsigned long long)dc);
         if (b == sp.nval + 1) {
             atomicAdd(&cnt->items, (unsigned long long)nparts_of(k, sp.part_cap));
         } else if (b == sp.nval + 2) {
@@ -243,13 +253,15 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         }
         lists[bin_start[b] + within] = ref;
         if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
-        if (spec.dcap[b] > 0) dup_off[r] = (int64_t)atomicAdd(&cnt->dup_cur, (unsigned long long)spec.dcap[b]);
+        const int32_t dc = dcap_of(spec, b, k);
+        if (dc > 0) dup_off[r] = (int64_t)atomicAdd(&cnt->dup_cur, (unsigned long long)dc);
         if (b == part_bin) {
             const uint32_t np = nparts_of(k, spec.part_cap);
             const unsigned long long at = atomicAdd(&cnt->items_cur, (unsigned long long)np);
             for (uint32_t q = 0; q < np; ++q) items[at + q] = PartItem{ref, q, np};
             if (spec.zero_nnz) nnz_row[r] = 0;
-            if (dupn) dupn[r] = -1;   // partitioned rows take the table path
+            // partitioned rows: a duplicate counter (k_dup_place decides the path)
+            if (dupn) dupn[r] = spec.part_dcap_div > 0 ? 0 : -1;
         } else if (b == wide_bin) {
             const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
             unsigned long long S = 1;
@@ -373,7 +385,9 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
 // (added to nnz_row) and the first-touch bits of the row's bitmap.
 template <int TEAM, int K, int LOG2S>
 __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, const PartItem *items,
-                                                        Bitmap bm, int32_t *nnz_row, int *overflow) {
+                                                        Bitmap bm, int32_t *nnz_row, uint2 *gpairs,
+                                                        const int64_t *dup_off, int32_t *dupn,
+                                                        int32_t div, int32_t dmax, int *overflow) {
     __shared__ int32_t keys[1 << LOG2S];
     __shared__ uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
@@ -383,8 +397,10 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
     SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
+    const uint32_t cap = div > 0 ? (uint32_t)min(it.ref.n / div, dmax) : 0u;
     const int32_t n = symbolic_part_row<TEAM, K>(tcol, it.ref, tb, it.part, it.nparts, scratch, lbits,
-                                                 gbits, overflow);
+                                                 gbits, cap > 0 ? gpairs + dup_off[row] : nullptr,
+                                                 dupn + row, cap, overflow);
     // publish this partition's first-touch words (one atomic per non-zero word)
     const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)it.ref.n + 31) / 32);
     for (int64_t w = threadIdx.x; w < W; w += TEAM)
@@ -408,6 +424,32 @@ __global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32
         const int ex = Team<256>::excl_sum(c, tot, scratch);
         if (w < W) pref[w] = (uint32_t)(carry + ex);
         carry += tot;
+    }
+}
+
+// Partitioned rows: place the unordered duplicate pairs at their product-
+// order index d = p - rank(p) (bitmap complete), or send the row to the
+// table path when its duplicates overflowed its list.
+__global__ __launch_bounds__(256) void k_dup_place(const RowRef *list, int32_t count, Bitmap bm,
+                                                   const uint2 *gpairs, const int64_t *dup_off,
+                                                   int32_t *dupn, int32_t *gdupt, int32_t div,
+                                                   int32_t dmax) {
+    const RowRef ref = list[blockIdx.x];
+    const int64_t row = ref.row;
+    const int32_t cnt = dupn[row];
+    const int32_t cap = div > 0 ? min(ref.n / div, dmax) : 0;
+    if (cnt > cap) {
+        if (threadIdx.x == 0) dupn[row] = -1;
+        return;
+    }
+    const uint32_t *bits = bm.bits + bm.off[row];
+    const uint32_t *pref = bm.pref + bm.off[row];
+    const uint2 *pr = gpairs + dup_off[row];
+    int32_t *dt = gdupt + dup_off[row];
+    for (int32_t i = threadIdx.x; i < cnt; i += 256) {
+        const uint2 e = pr[i];
+        const uint32_t rk = pref[e.x >> 5] + (uint32_t)__popc(bits[e.x >> 5] & ((1u << (e.x & 31)) - 1u));
+        dt[e.x - rk] = (int32_t)e.y;
     }
 }
 
@@ -507,6 +549,20 @@ __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int
     const int64_t off = bm.off[row];
     numeric_fixup_row<WAVE>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
                             gdupval + dup_off[row], nd, dupt[team], out);
+}
+
+// Duplicate fix-up of streaming rows with long duplicate lists (sort-based).
+constexpr int FIXBIG_CAP = 8192;
+__global__ __launch_bounds__(1024) void k_fixup_big(const RowRef *list, int32_t count, Bitmap bm,
+                                                   const int64_t *dup_off, const int32_t *dupn,
+                                                   const int32_t *gdupt, const double *gdupval, Out out) {
+    __shared__ unsigned long long key[FIXBIG_CAP];
+    const int64_t row = list[blockIdx.x].row;
+    const int32_t nd = dupn[row];
+    if (nd <= 0 || nd > FIXBIG_CAP) return;
+    const int64_t off = bm.off[row];
+    numeric_fixup_big<1024>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row], gdupval + dup_off[row],
+                            nd, key, FIXBIG_CAP, out);
 }
 
 // Row-wise analysis helpers: product offset of every row, and the expansion
@@ -893,7 +949,7 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
-static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 4 <= MAX_BINS, "bins");
+static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 5 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
 // first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
@@ -901,8 +957,9 @@ static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upp
 // duplicate-list capacity of a symbolic bin: rows with more duplicate
 // products than this take the table path in the numeric pass
 static constexpr int32_t dcap_for(int32_t upper) {
-    return upper / 8 < 8 ? 8 : (upper / 8 > 256 ? 256 : upper / 8);
+    return upper / 8 < 8 ? 8 : (upper / 8 > 1024 ? 1024 : upper / 8);
 }
+constexpr int32_t PART_DCAP_DIV = 8;   // partitioned rows: list of min(products / 8, FIXBIG_CAP)
 
 // TEAM * PER of each value configuration in val_bin(): the emission loop
 // visits that many slots, so it must cover every bin's S.
@@ -925,6 +982,8 @@ static BinSpec sym_spec() {
     s.ratio_num = 0;
     s.ratio_den = 0;
     s.part_cap = SYM_PART_CAP;
+    s.part_dcap_div = PART_DCAP_DIV;
+    s.part_dcap_max = FIXBIG_CAP;
     s.wide_min = 0;
     s.ft = 1;
     s.zero_nnz = 1;
@@ -937,8 +996,8 @@ static BinSpec num_spec() {
     s.ndw = N_DW;
     for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
     for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
-    // streaming rows: one bin, the rows that need a duplicate fix-up
-    s.nst = 1;
+    // streaming rows: the rows that need a duplicate fix-up (short, long lists)
+    s.nst = 2;
     s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
     s.ratio_den = 2;
     s.part_cap = NUM_PART_CAP;
@@ -1291,6 +1350,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_BPREF, sizeof(uint32_t) * (c1.bm_words + 1)));
     IAS_TRY(reserve(B_DUPT, sizeof(int32_t) * (c1.dup_slots + 1)));
     IAS_TRY(reserve(B_DUPV, sizeof(double) * (c1.dup_slots + 1)));
+    IAS_TRY(reserve(B_DUPP, sizeof(uint2) * (c1.dup_slots + 1)));
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
     if (c1.count[sym_part] > 0) HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
@@ -1310,8 +1370,11 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
         k_symbolic_part<1024, 4, 14><<<(unsigned)c1.items, 1024, 0, t>>>(
-            tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, &dc2->overflow);
+            tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
+            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow);
         k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+        k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
+                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
     for (int b = ss.nval; b >= 1; --b)
@@ -1435,6 +1498,11 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             k_fixup<<<grid_for(c, FIX_TPW), WAVE * FIX_TPW, 0, t>>>(NL + st[fb], c, bm, sa.dup_off, sa.dupn,
                                                                    sa.dupt, as<double>(bufs[B_DUPV]), out);
             CHECK_LAUNCH("k_fixup", t);
+        }
+        if ((c = num_count[fb + 1]) > 0) {
+            k_fixup_big<<<c, 1024, 0, t>>>(NL + st[fb + 1], c, bm, sa.dup_off, sa.dupn, sa.dupt,
+                                           as<double>(bufs[B_DUPV]), out);
+            CHECK_LAUNCH("k_fixup_big", t);
         }
     }
     for (int b = ns.nval; b >= 1; --b)

@@ -23,6 +23,8 @@ struct BinSpec {
     int32_t part_cap;          // keys per hash partition in bin nval+1
     int32_t wide_min;          // key >= wide_min -> bin nval+2 (0: never)
     int32_t dcap[MAX_BINS];    // duplicate-list capacity per LDS bin (symbolic; 0: none)
+    int32_t part_dcap_div;     // partitioned rows: duplicate list of min(key / div, max) (0: none)
+    int32_t part_dcap_max;
     int32_t ft;                // give every listed row a first-touch bitmap
     int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
 };
@@ -49,7 +51,7 @@ struct Counters {
 struct ias_plan {
     enum {
         B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
-        B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT,
+        B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
     };
     struct Buf {

@@ -480,13 +480,19 @@ __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t 
 
 // One team counts the distinct columns of one hash partition of a row whose
 // products are tcol[ref.q0 .. ref.q0 + ref.n), with the first-touch position
-// of every column published as bits of the row's bitmap.  Returns the team's
-// count; *overflow is set when the table filled up.
+// of every column published as bits of the row's bitmap.  Duplicates (a
+// product whose column was touched first by an earlier product — all of a
+// column's products fall in one partition) are appended unordered as
+// (product, first touch) pairs to the row's list `pairs` through the row's
+// counter *dcnt (one atomic per wave and step); entries beyond `cap` are
+// counted but not stored.  Returns the team's count; *overflow is set when
+// the table filled up.
 template <int TEAM, int K>
 __device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const RowRef &ref,
                                                      const SymTable<true> &table, uint32_t part,
                                                      uint32_t nparts, int *scratch, uint32_t *lbits,
-                                                     uint32_t *gbits, int *overflow) {
+                                                     uint32_t *gbits, uint2 *pairs, int32_t *dcnt,
+                                                     uint32_t cap, int *overflow) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = table.size;
@@ -513,6 +519,21 @@ __device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const 
 #pragma unroll
         for (int k = 0; k < K; ++k) use[k] = c[k] != EMPTY_KEY && part_of(c[k], nparts) == part;
         insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
+        if (pairs) {
+            TM::sync();   // first touches of this step's columns are final
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t m = slot[k] >= 0 ? table.minp[slot[k]] : 0u;
+                const bool dup = slot[k] >= 0 && m != pp[k];
+                const uint64_t b = __ballot(dup);
+                if (b == 0ull) continue;
+                int base = 0;
+                if ((__lane_id()) == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(dcnt, __popcll(b));
+                base = __shfl(base, __builtin_ctzll(b));
+                const uint32_t i = (uint32_t)base + (uint32_t)__popcll(b & ((1ull << __lane_id()) - 1ull));
+                if (dup && i < cap) pairs[i] = make_uint2(pp[k], m);
+            }
+        }
     }
     TM::sync();
     for (uint32_t s = lane; s < S; s += TEAM)
@@ -809,6 +830,52 @@ __device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *b
             if (dupt[j] == t) v = v + gdupval[j];
         out.val[pos] = v;
     }
+}
+
+// Fix-up of a streaming row with many duplicates (more than one wave's
+// list): (first touch, index) keys sorted in LDS (bitonic, nd <= cap2 = a
+// power of two), then each run of equal first touches adds its products to
+// its entry in product order (sorted by index within the run).
+template <int TEAM>
+__device__ __forceinline__ void numeric_fixup_big(int64_t row, const uint32_t *bits, const uint32_t *bpref,
+                                                  const int32_t *gdupt, const double *gdupval,
+                                                  int32_t ndup, unsigned long long *key, uint32_t cap2,
+                                                  const Out &out) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    uint32_t n2 = 1;
+    while (n2 < (uint32_t)ndup) n2 <<= 1;
+    for (uint32_t i = lane; i < n2; i += TEAM)
+        key[i] = i < (uint32_t)ndup ? (((unsigned long long)(uint32_t)gdupt[i] << 32) | i) : ~0ull;
+    TM::sync();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < n2; i += TEAM) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = key[i], b = key[ixj];
+                    if ((a > b) == ((i & k) == 0)) {
+                        key[i] = b;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            TM::sync();
+        }
+    }
+    const int64_t st = out.start(row);
+    const uint32_t nnz = (uint32_t)out.len[row];
+    for (uint32_t i = lane; i < (uint32_t)ndup; i += TEAM) {
+        const uint32_t t = (uint32_t)(key[i] >> 32);
+        if (i > 0 && (uint32_t)(key[i - 1] >> 32) == t) continue;
+        const uint32_t rk = bpref[t >> 5] + (uint32_t)__popc(bits[t >> 5] & ((1u << (t & 31)) - 1u));
+        const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+        double v = out.val[pos];
+        for (uint32_t j = i; j < (uint32_t)ndup && (uint32_t)(key[j] >> 32) == t; ++j)
+            v = v + gdupval[(uint32_t)key[j]];
+        out.val[pos] = v;
+    }
+    (void)cap2;
 }
 
 // ---------------------------------------------------------------- numeric
