@@ -28,9 +28,9 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
 // stv duplicates -> the fix-up bin when it has any, nothing to do otherwise).
 __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv) {
     if (k <= 0) return 0;
-    if (stv >= 0 && sp.nst > 0) {   // fix-up bins: short lists (one wave), long lists (sorted)
+    if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), longer (sorted)
         if (stv == 0) return 0;
-        return sp.nval + 3 + sp.ndw + (stv > 256 ? 1 : 0);
+        return sp.nval + 3 + sp.ndw + (stv > 256 ? 2 : (stv > 16 ? 1 : 0));
     }
     if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
     const bool val_class =
@@ -551,6 +551,49 @@ __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int
                             gdupval + dup_off[row], nd, dupt[team], out);
 }
 
+// Duplicate fix-up of streaming rows with short lists (<= 16): one lane per
+// row, the list in registers, each column's products added in list order.
+constexpr int FIX_TINY = 16;
+__global__ __launch_bounds__(256) void k_fixup_tiny(const RowRef *list, int32_t count, Bitmap bm,
+                                                    const int64_t *dup_off, const int32_t *dupn,
+                                                    const int32_t *gdupt, const double *gdupval, Out out) {
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= count) return;
+    const int64_t row = list[idx].row;
+    const int32_t nd = dupn[row];
+    if (nd <= 0 || nd > FIX_TINY) return;
+    const int64_t off = dup_off[row];
+    const uint32_t *bits = bm.bits + bm.off[row];
+    const uint32_t *pref = bm.pref + bm.off[row];
+    int32_t t[FIX_TINY];
+    double v[FIX_TINY];
+#pragma unroll
+    for (int i = 0; i < FIX_TINY; ++i)
+        if (i < nd) {
+            t[i] = gdupt[off + i];
+            v[i] = gdupval[off + i];
+        }
+    const int64_t st = out.start(row);
+    const uint32_t nnz = (uint32_t)out.len[row];
+#pragma unroll
+    for (int i = 0; i < FIX_TINY; ++i) {
+        if (i >= nd) break;
+        bool head = true;
+#pragma unroll
+        for (int j = 0; j < FIX_TINY; ++j)
+            if (j < i && t[j] == t[i]) head = false;
+        if (!head) continue;
+        const uint32_t p = (uint32_t)t[i];
+        const uint32_t rk = pref[p >> 5] + (uint32_t)__popc(bits[p >> 5] & ((1u << (p & 31)) - 1u));
+        const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+        double a = out.val[pos];
+#pragma unroll
+        for (int j = 0; j < FIX_TINY; ++j)
+            if (j >= i && j < nd && t[j] == t[i]) a = a + v[j];
+        out.val[pos] = a;
+    }
+}
+
 // Duplicate fix-up of streaming rows with long duplicate lists (sort-based).
 constexpr int FIXBIG_CAP = 8192;
 __global__ __launch_bounds__(1024) void k_fixup_big(const RowRef *list, int32_t count, Bitmap bm,
@@ -949,7 +992,7 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
-static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 5 <= MAX_BINS, "bins");
+static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
 
 static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
 // first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
@@ -996,8 +1039,8 @@ static BinSpec num_spec() {
     s.ndw = N_DW;
     for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
     for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
-    // streaming rows: the rows that need a duplicate fix-up (short, long lists)
-    s.nst = 2;
+    // streaming rows: the rows that need a duplicate fix-up (by list length)
+    s.nst = 3;
     s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
     s.ratio_den = 2;
     s.part_cap = NUM_PART_CAP;
@@ -1369,7 +1412,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int lane_no = 0;
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        k_symbolic_part<1024, 4, 14><<<(unsigned)c1.items, 1024, 0, t>>>(
+        k_symbolic_part<1024, 8, 14><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
             PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow);
         k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
@@ -1495,12 +1538,18 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         CHECK_LAUNCH("k_numeric_flat", t);
         const int fb = ns.nval + 3 + N_DW;
         if ((c = num_count[fb]) > 0) {
-            k_fixup<<<grid_for(c, FIX_TPW), WAVE * FIX_TPW, 0, t>>>(NL + st[fb], c, bm, sa.dup_off, sa.dupn,
-                                                                   sa.dupt, as<double>(bufs[B_DUPV]), out);
-            CHECK_LAUNCH("k_fixup", t);
+            k_fixup_tiny<<<grid_for(c, 256), 256, 0, t>>>(NL + st[fb], c, bm, sa.dup_off, sa.dupn, sa.dupt,
+                                                          as<double>(bufs[B_DUPV]), out);
+            CHECK_LAUNCH("k_fixup_tiny", t);
         }
         if ((c = num_count[fb + 1]) > 0) {
-            k_fixup_big<<<c, 1024, 0, t>>>(NL + st[fb + 1], c, bm, sa.dup_off, sa.dupn, sa.dupt,
+            k_fixup<<<grid_for(c, FIX_TPW), WAVE * FIX_TPW, 0, t>>>(NL + st[fb + 1], c, bm, sa.dup_off,
+                                                                   sa.dupn, sa.dupt, as<double>(bufs[B_DUPV]),
+                                                                   out);
+            CHECK_LAUNCH("k_fixup", t);
+        }
+        if ((c = num_count[fb + 2]) > 0) {
+            k_fixup_big<<<c, 1024, 0, t>>>(NL + st[fb + 2], c, bm, sa.dup_off, sa.dupn, sa.dupt,
                                            as<double>(bufs[B_DUPV]), out);
             CHECK_LAUNCH("k_fixup_big", t);
         }
