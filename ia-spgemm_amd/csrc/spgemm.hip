@@ -388,7 +388,7 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
                                                         Bitmap bm, int32_t *nnz_row, uint2 *gpairs,
                                                         const int64_t *dup_off, int32_t *dupn,
                                                         int32_t div, int32_t dmax, int *overflow) {
-    __shared__ int32_t keys[1 << LOG2S];
+    __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
     __shared__ uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_numeric_dw(AxView ax, Rows B, con
 template <int TEAM, int K, int LOG2S, int SEG>
 __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const PartItem *items,
                                                        Bitmap bm, Out out, int *overflow) {
-    __shared__ int32_t keys[1 << LOG2S];
+    __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
     __shared__ uint32_t meta[1 << LOG2S];
     __shared__ Seg<SEG, true> seg;
     __shared__ int scratch[64];
@@ -994,7 +994,8 @@ constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
 static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
 
-static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)((3ll * upper + 1) / 2); }
+// table slots of an LDS bin: 1.5 x its bound, a whole number of 4-slot buckets
+static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)(((3ll * upper + 1) / 2 + 3) / 4 * 4); }
 // first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
 static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upper + 63) / 64)); }
 // duplicate-list capacity of a symbolic bin: rows with more duplicate

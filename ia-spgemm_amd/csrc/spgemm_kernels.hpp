@@ -458,22 +458,46 @@ __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t 
     for (int k = 0; k < K; ++k)
         if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
 #else
+    // Bucketed probing: the home position is a 16-byte bucket of 4 slots,
+    // read with one LDS load; the column is found in it, or CASed into its
+    // first empty slot, or the probe moves to the next bucket.  Linear
+    // probing over single slots left long probe tails at load 1/2..2/3, and
+    // a wave waits for its slowest lane (S is a multiple of 4).
+    const uint32_t nb = S >> 2;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         slot[k] = -1;
         if (!use[k]) continue;
-        uint32_t s = slot_hash(c[k], S);
+        uint32_t b = slot_hash(c[k], nb);
         for (uint32_t probe = 0; probe < S; ++probe) {
-            const int32_t v = atomicCAS(&key[s], EMPTY_KEY, c[k]);
-            if (v == EMPTY_KEY || v == c[k]) {
-                created += v == EMPTY_KEY ? 1 : 0;
-                atomicMin(&minp[s], p[k]);
-                slot[k] = (int)s;
+            const int4 q = ((const int4 *)key)[b];
+            int hit = -1, empty = -1;
+            if (q.w == c[k]) hit = 3;
+            if (q.z == c[k]) hit = 2;
+            if (q.y == c[k]) hit = 1;
+            if (q.x == c[k]) hit = 0;
+            if (q.w == EMPTY_KEY) empty = 3;
+            if (q.z == EMPTY_KEY) empty = 2;
+            if (q.y == EMPTY_KEY) empty = 1;
+            if (q.x == EMPTY_KEY) empty = 0;
+            if (hit >= 0) {
+                slot[k] = (int)(4 * b + hit);
                 break;
             }
-            s = (s + 1u == S) ? 0u : s + 1u;
+            if (empty < 0) {
+                b = (b + 1u == nb) ? 0u : b + 1u;
+                continue;
+            }
+            const int32_t v = atomicCAS(&key[4 * b + empty], EMPTY_KEY, c[k]);
+            if (v == EMPTY_KEY || v == c[k]) {
+                created += v == EMPTY_KEY ? 1 : 0;
+                slot[k] = (int)(4 * b + empty);
+                break;
+            }
+            // another column took that slot: re-read the same bucket
         }
-        if (slot[k] < 0) full = true;
+        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
+        else full = true;
     }
 #endif
 }

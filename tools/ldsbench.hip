@@ -94,6 +94,23 @@ __global__ __launch_bounds__(256) void hash_ins(int rows, int n, unsigned long l
     if (created == -1) sink[0] = created;
 }
 
+// dependent LDS CAS chain latency vs waves per CU (one block of `threads` per CU)
+__global__ void cas_chain(int iters, unsigned long long *sink, unsigned long long *cyc) {
+    __shared__ uint32_t t[8192];
+    for (int i = threadIdx.x; i < 8192; i += blockDim.x) t[i] = 0;
+    __syncthreads();
+    uint32_t h = threadIdx.x * 0x9E3779B1u + 12345u;
+    const unsigned long long t0 = wall_clock64();
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t s = (h >> 7) & 8191u;
+        const uint32_t v = atomicCAS(&t[s], 0u, h | 1u);
+        h = h * 1664525u + 1013904223u + v;
+    }
+    const unsigned long long t1 = wall_clock64();
+    if (threadIdx.x == 0 && blockIdx.x == 0) cyc[0] = t1 - t0;
+    if (h == 7) sink[0] = h;
+}
+
 int main() {
     unsigned long long *sink;
     hipMalloc(&sink, 8);
@@ -129,6 +146,19 @@ int main() {
         const double ops = (double)cus * 2 * 1024 * iters;
         printf("%-24s %.2f lane-ops/clk/CU (at 2.4 GHz), %.1f G lane-ops/s\n", names[op],
                ops / (ms * 1e-3) / cus / 2.4e9, ops / (ms * 1e-3) / 1e9);
+    }
+    {
+        unsigned long long *cyc;
+        hipMalloc(&cyc, 8);
+        for (int thr : {64, 256, 512, 1024}) {
+            const int iters = 2000;
+            cas_chain<<<cus, thr>>>(iters, sink, cyc);
+            cas_chain<<<cus, thr>>>(iters, sink, cyc);
+            unsigned long long h;
+            hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost);
+            printf("dependent CAS chain, %2d waves/CU: %.0f ns per CAS (%.0f clocks at 2.4 GHz)\n", thr / 64,
+                   h * 10.0 / iters, h * 10.0 / iters * 2.4);
+        }
     }
     for (int n : {64, 512, 2048}) {
         for (int mode = 0; mode < 3; ++mode) {
