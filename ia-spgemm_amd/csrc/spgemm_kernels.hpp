@@ -649,29 +649,38 @@ __device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const Ro
         // steps only bring larger products, so no second barrier is needed).
         // Duplicates are listed unordered; their product-order index comes
         // from the finished bitmap (d = p - rank(p)).
+        bool ft[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k) {
+            ft[k] = false;
             if (slot[k] >= 0) {
                 const uint32_t m = table.minp[slot[k]];
-                if (m != pp[k]) {
+                ft[k] = m == pp[k];
+                if (!ft[k]) {
                     const int i = atomicAdd(dcount, 1);
                     if ((uint32_t)i < dcap) dups[i] = make_uint2(pp[k], m);
                 }
             }
-        tm.mark(4);
-    }
-    TM::sync();
-    {   // first-touch bits from the table, 4 slots per lane-read
-        const uint4 *k4 = (const uint4 *)table.key;
-        const uint4 *m4 = (const uint4 *)table.minp;
-        for (uint32_t i = lane; i < (S + 3) / 4; i += TEAM) {
-            const uint4 kk = k4[i];
-            const uint4 mm = m4[i];
-            if ((int32_t)kk.x != EMPTY_KEY) atomicOr(&lbits[mm.x >> 5], 1u << (mm.x & 31));
-            if ((int32_t)kk.y != EMPTY_KEY) atomicOr(&lbits[mm.y >> 5], 1u << (mm.y & 31));
-            if ((int32_t)kk.z != EMPTY_KEY) atomicOr(&lbits[mm.z >> 5], 1u << (mm.z & 31));
-            if ((int32_t)kk.w != EMPTY_KEY) atomicOr(&lbits[mm.w >> 5], 1u << (mm.w & 31));
         }
+        // first-touch bits straight from ballots (items of one k and one wave
+        // are 64 consecutive products), no scan of the table afterwards
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const uint64_t bal = __ballot(ft[k]);
+            const uint32_t base = (uint32_t)(p0 + k * TEAM);
+            if constexpr (TEAM >= WAVE) {
+                const uint32_t wb = base + (uint32_t)(lane & ~(WAVE - 1));   // 64-aligned
+                if ((lane & (WAVE - 1)) == 0 && wb < (uint32_t)P) {
+                    lbits[wb >> 5] = (uint32_t)bal;
+                    lbits[(wb >> 5) + 1] = (uint32_t)(bal >> 32);
+                }
+            } else {
+                const int tb = (int)(__lane_id() & ~(TEAM - 1));
+                const uint32_t bits = (uint32_t)((bal >> tb) & ((1ull << TEAM) - 1ull));
+                if (lane == 0 && bits) atomicOr(&lbits[base >> 5], bits << (base & 31));
+            }
+        }
+        tm.mark(4);
     }
     TM::sync();
     ndup = (uint32_t)*dcount;
