@@ -995,7 +995,20 @@ constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
 static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
 
 // table slots of an LDS bin: 1.5 x its bound, a whole number of 4-slot buckets
-static constexpr uint32_t slots_for(int32_t upper) { return (uint32_t)(((3ll * upper + 1) / 2 + 3) / 4 * 4); }
+#ifndef SLOT_NUM
+#define SLOT_NUM 3   // slots per bound: SLOT_NUM / 2
+#endif
+static constexpr uint32_t slots_for(int32_t upper) {
+    return (uint32_t)(((SLOT_NUM * (long long)upper + 1) / 2 + 3) / 4 * 4);
+}
+// symbolic LDS bins may use a lower load where LDS is not the limit
+#ifndef SYM_SLOT_NUM_SMALL
+#define SYM_SLOT_NUM_SMALL 3
+#endif
+static constexpr uint32_t sym_slots_for(int32_t upper) {
+    return upper <= 1024 ? (uint32_t)(((SYM_SLOT_NUM_SMALL * (long long)upper + 1) / 2 + 3) / 4 * 4)
+                         : slots_for(upper);
+}
 // first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
 static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upper + 63) / 64)); }
 // duplicate-list capacity of a symbolic bin: rows with more duplicate
@@ -1128,12 +1141,15 @@ static void sym_launch(const Launch &l, const int32_t *tcol, uint32_t W, uint32_
                                                    a.dupn, a.dupt);
 }
 
+#ifndef SYM_WPE_SMALL
+#define SYM_WPE_SMALL 7   // waves per SIMD the register budget of the wave-level teams allows
+#endif
 static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, uint32_t D, int32_t *nnz,
                     const StArgs &a) {
     switch (cfg) {
-        case 0: sym_launch<16, 4, 16, 6>(l, tcol, W, D, nnz, a); break;
-        case 1: sym_launch<32, 4, 8, 6>(l, tcol, W, D, nnz, a); break;
-        case 2: sym_launch<64, 4, 4, 6>(l, tcol, W, D, nnz, a); break;
+        case 0: sym_launch<16, 4, 16, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
+        case 1: sym_launch<32, 4, 8, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
+        case 2: sym_launch<64, 4, 4, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
         case 3: sym_launch<64, 8, 4, 4>(l, tcol, W, D, nnz, a); break;
         case 4: sym_launch<128, 4, 1, 6>(l, tcol, W, D, nnz, a); break;
         case 5: sym_launch<256, 4, 1, 1>(l, tcol, W, D, nnz, a); break;
@@ -1425,7 +1441,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
             const int32_t u = SYM_BINS[b - 1].upper;
-            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, slots_for(u), t, ax, B, SL + st[b]}, tcol, words_for(u),
+            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, sym_slots_for(u), t, ax, B, SL + st[b]}, tcol, words_for(u),
                     (uint32_t)dcap_for(u), nnz, sa);
             CHECK_LAUNCH("k_symbolic_st", t);
         }

@@ -129,6 +129,61 @@ def test_csr_long_rows_global_tables():
     assert_csr_identical(got, ref, "long rows")
 
 
+def duplicate_tiers(seed=11):
+    """A·B whose first rows hit every duplicate-handling path: each A row i
+    takes m_i distinct rows of its own group of B, whose 100 columns are drawn
+    from a pool sized for the wanted duplicate count (d ~ P^2 / 2 pool):
+      P=1000 ~30 dups (one-wave fix-up), P=8000 ~500 (sorted fix-up, LDS bin),
+      P=30000 ~1800 (partitioned row, streaming), P=20000 ~5000 (partitioned
+      row beyond its list: table path), P=2000 ~500 (LDS row beyond its list:
+      direct-write table); then 2000 ordinary rows."""
+    rng = np.random.default_rng(seed)
+    per = 100
+    plan = [(1000, 16000), (8000, 64000), (30000, 250000), (20000, 40000), (2000, 3333)]
+    brows, arows = [], []
+    ncols = 300000
+    for prods, pool in plan:
+        m = prods // per
+        base = len(brows)
+        for _ in range(m):
+            brows.append(rng.choice(pool, per, replace=False))
+        arows.append(np.arange(base, base + m))
+    nb_special = len(brows)
+    for _ in range(4000):
+        brows.append(rng.choice(ncols, 12, replace=False))
+    for _ in range(2000):
+        arows.append(rng.choice(np.arange(nb_special, len(brows)), 8, replace=False))
+
+    def csr(rows, ncol):
+        rp = np.zeros(len(rows) + 1, np.int64)
+        rp[1:] = np.cumsum([len(r) for r in rows])
+        col = np.concatenate(rows).astype(np.int32)
+        val = rng.uniform(-1.0, 1.0, size=col.size)
+        return ias.HostCsr(len(rows), ncol, rp, col, val)
+
+    return csr(arows, len(brows)), csr(brows, ncols)
+
+
+def test_csr_duplicate_tiers():
+    A, B = duplicate_tiers()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    got, rep = ias.spgemm(A, B)
+    assert rep.max_row_products == 30000
+    assert_csr_identical(got, ref, "duplicate tiers")
+    # the same product through COO (forward first-touch order, first product assigned)
+    refc, ref_rows = ob.coo_mul_coo(ob.Mat.of(A), ob.Mat.of(B))
+    ca, cb, cc = _coo_of(A), _coo_of(B), ias.Coo()
+    o = ias.opts(output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_coo_mul_coo(C.byref(ca), C.byref(cb), C.byref(cc), C.byref(o), None), "coo")
+    n = cc.nnz
+    got_c = ias._np(cc.col, n, np.int32)
+    got_v = ias._np(cc.val, n, np.float64)
+    for m in (ca, cb, cc):
+        ias.lib.ias_coo_free(C.byref(m))
+    np.testing.assert_array_equal(got_c, refc.col)
+    np.testing.assert_array_equal(bits(got_v), bits(refc.val))
+
+
 def wide_row(n=1 << 20, head=1000, per=600):
     """Row 0 reaches head*per = 600k distinct columns: beyond the 19-bit rank
     field of the LDS/partition tables, so the 64-bit global-table path runs."""
