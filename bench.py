@@ -4,9 +4,12 @@
 Contract:
   python bench.py --gpus N --steps K --warmup W
 One step = one full C = A*A of this rank's row block through the C-ABI
-two-phase entry points (ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute:
-row analysis, binning, symbolic, scan, host read of nnz, numeric + write C),
-inputs resident in HBM, C written into preallocated device arrays.
+two-phase entry points (ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, as
+cuSPARSE's csrgemmNnz + csrgemm: row analysis, binning, symbolic, scan, host
+read of nnz, numeric + write C), inputs resident in HBM, C written into
+preallocated device arrays.  `--engine onepass` times the single-pass chunk
+engine instead (ias_csr_mul_csr_into with IAS_ONEPASS=1; C's capacity =
+flops(A*A) >= nnz(C), reported by a capacity-0 call before timing).
 
 Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15,
 edge factor 20, scale 20 + log2(N) — at N=1 this is the north-star headline
@@ -54,6 +57,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
+    p.add_argument("--engine", default="twophase", choices=["onepass", "twophase"])
     return p.parse_args()
 
 
@@ -145,9 +149,24 @@ def main():
     ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
     order = ias.ORDER_SORTED if args.order == "sorted" else ias.ORDER_REFERENCE
 
-    nnz_c = C.c_int64(0)
-    ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None, None), "nnz")
-    cap = int(nnz_c.value)
+    if args.engine == "onepass":
+        os.environ["IAS_ONEPASS"] = "1"
+    if args.engine == "twophase":
+        nnz_c = C.c_int64(0)
+        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None, None), "nnz")
+        cap = int(nnz_c.value)
+    else:
+        # capacity = flops of this shard (an upper bound of nnz(C) known from A and B alone):
+        # a capacity-0 call reports it without writing C
+        probe = ias.Report()
+        c_rp0 = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
+        C0 = ias.Csr(r1 - r0, cols, 0, C.cast(C.c_void_p(c_rp0.data_ptr()), ias.i64p), None, None,
+                     ias.MEMORY_DEVICE, local)
+        st = ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(C0), 0, C.byref(probe))
+        if st not in (0, 11):
+            ias.check(st, "into (capacity probe)")
+        cap = int(probe.flops)
+        del c_rp0
     c_rp = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
     c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
     c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
@@ -157,7 +176,13 @@ def main():
     rep = ias.Report()
     rep_s = ias.Report()
 
-    def step():
+    def step_onepass():
+        Cm.nnz = cap
+        ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
+                                               C.byref(rep)), "into")
+        return rep
+
+    def step_twophase():
         n = C.c_int64(0)
         ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None,
                                               C.byref(rep_s)), "nnz")
@@ -166,6 +191,8 @@ def main():
                                                   C.byref(rep)), "compute")
         rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
         return rep
+
+    step = step_onepass if args.engine == "onepass" else step_twophase
 
     for _ in range(args.warmup):
         step()
@@ -184,7 +211,8 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    nnz_tot = torch.tensor([float(cap)], dtype=torch.float64, device=dev)
+    local_nnz = int(Cm.nnz) if args.engine == "onepass" else cap
+    nnz_tot = torch.tensor([float(local_nnz)], dtype=torch.float64, device=dev)
     num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
     if dist_on:
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -195,25 +223,26 @@ def main():
     gflops = 2.0 * flops_total / (ms_step * 1e6)
     nnz_c_total = int(nnz_tot.item())
 
-    # Roofline (HBM-bound).  Dominant launch: k_numeric_flat,
-    # the numeric pass of the streaming rows (the largest single kernel of a
-    # step, event-timed on its own stream inside the library).  Its algorithmic
-    # bytes per launch: per product the column (4 B, from the expansion) and the
-    # B value (8 B), per C entry 12 B written.  The whole step's B_alg =
-    # bytes(A) + bytes(B) + bytes(C) over the step time is reported beside it.
+    # Roofline (HBM-bound).  Dominant launch: k_onepass, the
+    # chunk launch of the single pass (k_numeric_flat for --engine twophase),
+    # event-timed on its own stream inside the library.  Its algorithmic bytes
+    # per launch: per product the B column (4 B) and B value (8 B) gathered,
+    # per C entry 12 B written.  The whole step's B_alg = bytes(A) + bytes(B)
+    # + bytes(C) over the step time is reported beside it.
     rows_local = r1 - r0
     bytes_a = 8 * (rows_local + 1) + 12 * int(Am.nnz)
     bytes_b = 8 * (rows + 1) + 12 * nnz_a
-    bytes_c = 8 * (rows_local + 1) + 12 * cap
+    bytes_c = 8 * (rows_local + 1) + 12 * local_nnz
     alg_bytes = bytes_a + bytes_b + bytes_c
     ms_flat = statistics.mean(x[4] for x in reps)
     flat_bytes = 12 * int(rep.stream_products) + 12 * int(rep.stream_nnz)
     achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
+    kname = "k_onepass" if args.engine == "onepass" else "k_numeric_flat"
     traffic = None
     pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
     if os.path.exists(pmc_file):
         try:
-            traffic = json.load(open(pmc_file)).get("k_numeric_flat", {}).get("hbm_bytes_per_launch")
+            traffic = json.load(open(pmc_file)).get(kname, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -235,6 +264,7 @@ def main():
             "kind": kind, **prm,
             "rows": rows, "nnz_a": nnz_a, "flops": flops_total, "nnz_c": nnz_c_total,
             "order": args.order,
+            "engine": args.engine,
             "parallelism": f"row-block x{world_req}, B replicated",
         },
         "nnz_per_s": round(nnz_c_total / (ms_step * 1e-3), 1),
@@ -245,7 +275,7 @@ def main():
             "numeric": round(statistics.mean(x[3] for x in reps), 4),
         },
         "roofline": {
-            "kernel": "k_numeric_flat",
+            "kernel": kname,
             "bound": "hbm",
             "achieved": round(achieved, 1),
             "peak": HBM_PEAK_GBS,

@@ -401,6 +401,21 @@ int pick_device(const ias_opts &o, int a_mem, int a_dev) {
     return 0;
 }
 
+// IAS_ONEPASS=1 selects the single-pass chunk engine (onepass_kernels.hpp)
+// for CSR products; the default is the two-phase engine, faster on skewed
+// (power-law) inputs where most products sit in rows too long for a chunk.
+bool onepass_enabled() {
+    const char *e = getenv("IAS_ONEPASS");
+    return e && *e == '1';
+}
+
+// A C allocated at its upper bound (flops entries of 12 B) must leave room.
+bool onepass_fits(int64_t flops) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+    return 12.0 * (double)flops + 8.0 <= 0.5 * (double)fr;
+}
+
 double ms_since(hipEvent_t a, hipEvent_t b) {
     float t = 0;
     hipEventElapsedTime(&t, a, b);
@@ -437,15 +452,30 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     }
     dev::Rows ra{dA->row_ptr, nullptr, 0, dA->col, dA->val};
     dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
-    const int64_t nnz = plan->nnz_total;
-
     ias_csr D{};
-    IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
-    HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
-                        hipMemcpyDeviceToDevice, s));
-    dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0, nullptr};
-    ias_status stn = plan->numeric(ra, rb, out, rep);
+    ias_status stn = IAS_SUCCESS;
+    bool done = false;
+    plan->last_a = plan->last_b = nullptr;
+    if (onepass_enabled()) {
+        // single pass into C allocated at its upper bound flops(A*B) >= nnz(C)
+        IAS_TRY(plan->onepass_prepare(ra, rb, A->rows, B->cols, dA->nnz, rep));
+        if (onepass_fits(plan->flops)) {
+            IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, plan->flops, IAS_MEMORY_DEVICE, plan->device));
+            int64_t nnz = 0;
+            stn = plan->onepass_run(ra, rb, D.row_ptr, D.col, D.val, plan->flops, 0, 0, &nnz, rep);
+            D.nnz = nnz;
+            done = true;
+        }
+    }
+    if (!done) {
+        IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
+        const int64_t nnz = plan->nnz_total;
+        IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
+        HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                            hipMemcpyDeviceToDevice, s));
+        dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0, nullptr};
+        stn = plan->numeric(ra, rb, out, rep);
+    }
     if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
         stn = ias_sort_rows_device(plan, D.row_ptr, A->rows, D.col, D.val, plan->max_nnz);
     if (stn != IAS_SUCCESS) {
@@ -661,6 +691,52 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, plan->max_nnz));
     // C is complete when this returns (callers may read or free it at once,
     // from any stream), as the reference's timer sync does (GPU/detail/utime.h).
+    HIPC(hipStreamSynchronize(s));
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, const ias_csr *B, ias_csr *C,
+                                           int32_t order, ias_report *rep) {
+    if (!plan || !C) return IAS_ERROR_INVALID_ARGUMENT;
+    IAS_TRY(check_dev_csr(A, plan));
+    IAS_TRY(check_dev_csr(B, plan));
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    if (order != IAS_ORDER_REFERENCE && order != IAS_ORDER_SORTED) return IAS_ERROR_INVALID_ARGUMENT;
+    if (C->memory != IAS_MEMORY_DEVICE || C->device != plan->device || !C->row_ptr || C->nnz < 0 ||
+        (C->nnz > 0 && (!C->col || !C->val)))
+        return IAS_ERROR_INVALID_ARGUMENT;
+    if (rep) memset(rep, 0, sizeof *rep);
+    hipStream_t s = (hipStream_t)plan->stream;
+    HIPC(hipSetDevice(plan->device));
+    plan->last_a = plan->last_b = nullptr;   // the two-phase state is overwritten
+    dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
+    dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
+    C->rows = A->rows;
+    C->cols = B->cols;
+    int64_t nnz = 0;
+    if (onepass_enabled()) {
+        IAS_TRY(plan->onepass_prepare(ra, rb, A->rows, B->cols, A->nnz, rep));
+        const ias_status st = plan->onepass_run(ra, rb, C->row_ptr, C->col, C->val, C->nnz, 0, 0, &nnz, rep);
+        if (st == IAS_ERROR_INSUFFICIENT_CAPACITY) C->nnz = nnz;
+        IAS_TRY(st);
+    } else {
+        // two-phase engine behind the same call: nnz, then values when they fit
+        IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
+        nnz = plan->nnz_total;
+        HIPC(hipMemcpyAsync(C->row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                            hipMemcpyDeviceToDevice, s));
+        if (nnz > C->nnz) {
+            HIPC(hipStreamSynchronize(s));
+            set_last_error("C needs %lld entries, capacity %lld", (long long)nnz, (long long)C->nnz);
+            C->nnz = nnz;
+            return IAS_ERROR_INSUFFICIENT_CAPACITY;
+        }
+        dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0, nullptr};
+        IAS_TRY(plan->numeric(ra, rb, out, rep));
+    }
+    C->nnz = nnz;
+    if (order == IAS_ORDER_SORTED)
+        IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, 0));
     HIPC(hipStreamSynchronize(s));
     return IAS_SUCCESS;
 }

@@ -3,6 +3,7 @@
 // CUSP / cuSPARSE calls of GPU/main.cu:467-523).  See spgemm_kernels.hpp for
 // the per-row algorithm and DESIGN.md §4 for the pipeline and its roofline.
 #include "spgemm_kernels.hpp"
+#include "onepass_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
 
@@ -1254,6 +1255,8 @@ ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
 
 ias_plan::~ias_plan() {
     hipSetDevice(device);
+    delete sub;
+    sub = nullptr;
     if (stream) hipStreamSynchronize((hipStream_t)stream);
     for (auto &b : bufs)
         if (b.p) hipFree(b.p);
@@ -1268,6 +1271,7 @@ ias_plan::~ias_plan() {
     }
     if (fork_ev) hipEventDestroy(fork_ev);
     if (host_counters) hipHostFree(host_counters);
+    if (host_info) hipHostFree(host_info);
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
 }
 
@@ -1294,6 +1298,7 @@ ias_status ias_plan::init(int dev, void *strm) {
     const char *e = getenv("IAS_SERIAL");
     serial = e && *e && *e != '0';
     HIPC(hipHostMalloc(&host_counters, 2 * sizeof(Counters)));
+    HIPC(hipHostMalloc(&host_info, 64));
     return IAS_SUCCESS;
 }
 
@@ -1320,14 +1325,14 @@ AxView ias_plan::ax_view() {
     return AxView{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), as<double>(bufs[B_AXV])};
 }
 
-ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
-                              int64_t a_entries, ias_report *rep) {
-    (void)cols;
+// Analysis (queued, no host wait): products per row, expanded A, product
+// offsets per entry and per row, symbolic bin counts into the B_CNT counters.
+ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
     n_entries = a_entries;
-    const BinSpec ss = sym_spec(), ns = num_spec();
+    const BinSpec ss = sym_spec();
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
@@ -1352,8 +1357,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PART, sizeof(int64_t) * (nb + 2)));
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT2]);
-    Counters *hc = (Counters *)host_counters;
-    const AxView ax = ax_view();
 
     // ---- analysis: products per row, expanded A (+ product offsets), symbolic bin counts
     HIPC(hipEventRecord(ev[0], s));
@@ -1382,6 +1385,22 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff);
     CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
+    return IAS_SUCCESS;
+}
+
+ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
+                              int64_t a_entries, ias_report *rep) {
+    (void)cols;
+    IAS_TRY(analysis_launch(A, B, rows, a_entries));
+    hipStream_t s = (hipStream_t)stream;
+    const BinSpec ss = sym_spec(), ns = num_spec();
+    Counters *dc = as<Counters>(bufs[B_CNT]);
+    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Counters *hc = (Counters *)host_counters;
+    const AxView ax = ax_view();
+    int64_t *poff = as<int64_t>(bufs[B_POFF]);
+    const int64_t *axp = as<int64_t>(bufs[B_AXP]);
+    const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
@@ -1603,6 +1622,181 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         if (n_entries > 0 && hipEventElapsedTime(&f, ev[5], ev[6]) == hipSuccess) rep->ms_stream = f;
         rep->stream_products = st_prod;
         rep->stream_nnz = st_nnz;
+    }
+    return IAS_SUCCESS;
+}
+
+
+// =================================================================== single pass
+// Exclusive scan of n int32 values into out[0..n] (out[n] = total), on `s`.
+static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s) {
+    const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, nullptr);
+    k_scan_partials<<<1, 1024, 0, s>>>(part, nb);
+    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, out);
+}
+
+ias_status ias_plan::onepass_prepare(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
+                                     int64_t a_entries, ias_report *rep) {
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(hipSetDevice(device));
+    IAS_TRY(analysis_launch(A, B, rows, a_entries));
+    const size_t rn = (size_t)rows + 2;
+    IAS_TRY(reserve(B_OPCF, sizeof(int32_t) * rn));
+    IAS_TRY(reserve(B_OPBF, sizeof(int32_t) * rn));
+    IAS_TRY(reserve(B_OPCID, sizeof(int64_t) * rn));
+    IAS_TRY(reserve(B_OPBPOS, sizeof(int64_t) * rn));
+    IAS_TRY(reserve(B_OPCROW, sizeof(int64_t) * rn));
+    IAS_TRY(reserve(B_OPSTAT, sizeof(unsigned long long) * rn));
+    IAS_TRY(reserve(B_OPMISC, 256));
+    IAS_TRY(reserve(B_OPBROW, sizeof(int64_t) * rn));
+    IAS_TRY(reserve(B_OPBLEN, sizeof(int32_t) * rn));
+    IAS_TRY(reserve(B_OPBPTR, sizeof(int64_t) * rn));
+    int32_t *cf = as<int32_t>(bufs[B_OPCF]), *bf = as<int32_t>(bufs[B_OPBF]);
+    int64_t *cid = as<int64_t>(bufs[B_OPCID]), *bpos = as<int64_t>(bufs[B_OPBPOS]);
+    int64_t *crow = as<int64_t>(bufs[B_OPCROW]), *brow = as<int64_t>(bufs[B_OPBROW]);
+    int64_t *bptr = as<int64_t>(bufs[B_OPBPTR]);
+    int32_t *blen = as<int32_t>(bufs[B_OPBLEN]);
+    int32_t *misc = as<int32_t>(bufs[B_OPMISC]);   // [0] ticket, [1] nchunks
+    int64_t *part = as<int64_t>(bufs[B_PART]);
+    Counters *dc = as<Counters>(bufs[B_CNT]);
+    Counters *hc = (Counters *)host_counters;
+    int64_t *hi = (int64_t *)host_info;
+    if (rows > 0) {
+        k_op_flags<<<grid_for(rows, 256), 256, 0, s>>>(as<int64_t>(bufs[B_POFF]), as<int32_t>(bufs[B_PROD]), rows,
+                                                       cf, bf);
+        scan_i32(cf, rows, part, cid, s);
+        scan_i32(bf, rows, part, bpos, s);
+        k_op_lists<<<grid_for(rows, 256), 256, 0, s>>>(cf, cid, bf, bpos, rows, crow, misc + 1, brow);
+        k_op_biglen<<<grid_for(rows, 256), 256, 0, s>>>(A, bpos, brow, rows, blen);
+        scan_i32(blen, rows, part, bptr, s);
+        CHECK_LAUNCH("single-pass chunking", s);
+        HIPC(hipMemcpyAsync(hi, bpos + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipMemcpyAsync(hi + 1, bptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    } else {
+        hi[0] = hi[1] = 0;
+    }
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    const Counters c1 = *hc;
+    if (c1.overflow) {
+        set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
+        return IAS_ERROR_INVALID_ARGUMENT;
+    }
+    flops = (int64_t)c1.flops;
+    max_prod = c1.max_prod;
+    op_nbig = hi[0];
+    op_nbe = hi[1];
+    HIPC(hipEventRecord(ev[1], s));
+    if (op_nbig > 0) {
+        IAS_TRY(reserve(B_OPBCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(op_nbe, 1)));
+        IAS_TRY(reserve(B_OPBVAL, sizeof(double) * (size_t)std::max<int64_t>(op_nbe, 1)));
+        k_op_bigcopy<<<(unsigned)op_nbig, 256, 0, s>>>(A, brow, bptr, as<int32_t>(bufs[B_OPBCOL]),
+                                                        as<double>(bufs[B_OPBVAL]));
+        CHECK_LAUNCH("k_op_bigcopy", s);
+        if (!sub) {
+            sub = new ias_plan();
+            IAS_TRY(sub->init(device, stream));
+        }
+        const Rows ab{bptr, nullptr, 0, as<int32_t>(bufs[B_OPBCOL]), as<double>(bufs[B_OPBVAL])};
+        IAS_TRY(sub->symbolic(ab, B, op_nbig, cols, op_nbe, nullptr));
+    }
+    HIPC(hipEventRecord(ev[2], s));
+    if (rep) {
+        rep->flops = flops;
+        rep->max_row_products = max_prod;
+    }
+    return IAS_SUCCESS;
+}
+
+// IAS_OP_WAVES: workgroups per CU of the chunk launch (0 = occupancy).
+ias_status ias_plan::onepass_run(const Rows &A, const Rows &B, int64_t *c_ptr, int32_t *c_col, double *c_val,
+                                 int64_t cap, int32_t order, int32_t first_assign, int64_t *nnz_c,
+                                 ias_report *rep) {
+    hipStream_t s = (hipStream_t)stream;
+    HIPC(hipSetDevice(device));
+    const int64_t rows = n_rows;
+    int64_t *hi = (int64_t *)host_info;
+    int32_t *misc = as<int32_t>(bufs[B_OPMISC]);
+    if (rows <= 0) {
+        HIPC(hipMemsetAsync(c_ptr, 0, sizeof(int64_t), s));
+        HIPC(hipStreamSynchronize(s));
+        *nnz_c = 0;
+        return IAS_SUCCESS;
+    }
+    HIPC(hipMemsetAsync(bufs[B_OPSTAT].p, 0, sizeof(unsigned long long) * ((size_t)rows + 1), s));
+    HIPC(hipMemsetAsync(misc, 0, sizeof(int32_t), s));
+    OnepassArgs oa{A,
+                   B,
+                   ax_view(),
+                   as<int32_t>(bufs[B_AXR]),
+                   as<int64_t>(bufs[B_AXP]),
+                   as<int64_t>(bufs[B_POFF]),
+                   as<int32_t>(bufs[B_PROD]),
+                   as<int64_t>(bufs[B_OPCROW]),
+                   misc + 1,
+                   op_nbig > 0 ? (const int32_t *)sub->bufs[B_NNZ].p : nullptr,
+                   as<int64_t>(bufs[B_OPBPOS]),
+                   as<unsigned long long>(bufs[B_OPSTAT]),
+                   misc,
+                   c_ptr,
+                   c_col,
+                   c_val,
+                   rows,
+                   cap,
+                   order,
+                   first_assign};
+    auto kern = k_onepass<OP_BLOCK, OP_NPM>;
+    int64_t grid = resident_blocks(kern, OP_BLOCK, 0);
+    grid = std::max<int64_t>(1, std::min<int64_t>(grid, rows));
+    HIPC(hipEventRecord(ev[5], s));
+    kern<<<(unsigned)grid, OP_BLOCK, 0, s>>>(oa);
+    HIPC(hipEventRecord(ev[6], s));
+    CHECK_LAUNCH("k_onepass", s);
+    HIPC(hipMemcpyAsync(hi + 2, c_ptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    nnz_total = hi[2];
+    *nnz_c = nnz_total;
+    if (nnz_total > cap) {
+        set_last_error("C needs %lld entries, capacity %lld", (long long)nnz_total, (long long)cap);
+        return IAS_ERROR_INSUFFICIENT_CAPACITY;
+    }
+    if (op_nbig > 0) {
+        IAS_TRY(reserve(B_OPBCPTR, sizeof(int64_t) * ((size_t)op_nbig + 1)));
+        int64_t *bcptr = as<int64_t>(bufs[B_OPBCPTR]);
+        k_op_bigptr<<<grid_for(op_nbig, 256), 256, 0, s>>>(c_ptr, as<int64_t>(bufs[B_OPBROW]), op_nbig, bcptr);
+        const Rows ab{as<int64_t>(bufs[B_OPBPTR]), nullptr, 0, as<int32_t>(bufs[B_OPBCOL]),
+                      as<double>(bufs[B_OPBVAL])};
+        const Out out{bcptr, 0, c_col, c_val, nullptr, order, first_assign, nullptr};
+        IAS_TRY(sub->numeric(ab, B, out, nullptr));
+    }
+    HIPC(hipEventRecord(ev[4], s));
+    if (rep) {
+        HIPC(hipMemsetAsync(misc + 2, 0, sizeof(int32_t), s));
+        k_op_maxlen<<<grid_for(rows, 256), 256, 0, s>>>(c_ptr, rows, misc + 2);
+        HIPC(hipMemcpyAsync((int32_t *)(hi + 3), misc + 2, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    }
+    HIPC(hipStreamSynchronize(s));
+    if (rep) {
+        max_nnz = *(int32_t *)(hi + 3);
+        rep->max_row_nnz = max_nnz;
+        float a = 0, b = 0, n = 0, t = 0, f = 0;
+        hipEventElapsedTime(&a, ev[0], ev[1]);
+        hipEventElapsedTime(&b, ev[1], ev[2]);
+        hipEventElapsedTime(&n, ev[2], ev[4]);
+        hipEventElapsedTime(&t, ev[0], ev[4]);
+        hipEventElapsedTime(&f, ev[5], ev[6]);
+        rep->ms_analysis = a;
+        rep->ms_symbolic = b;
+        rep->ms_numeric = n;
+        rep->ms_total = t;
+        rep->ms_stream = f;
+        rep->flops = flops;
+        rep->nnz_c = nnz_total;
+        rep->max_row_products = max_prod;
+        rep->stream_products = flops - (op_nbig > 0 ? sub->flops : 0);
+        rep->stream_nnz = nnz_total - (op_nbig > 0 ? sub->nnz_total : 0);
     }
     return IAS_SUCCESS;
 }

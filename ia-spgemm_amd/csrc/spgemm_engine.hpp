@@ -52,7 +52,10 @@ struct ias_plan {
     enum {
         B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
-        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_COUNT
+        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4,
+        // single-pass path (onepass)
+        B_OPCF, B_OPBF, B_OPCID, B_OPBPOS, B_OPCROW, B_OPSTAT, B_OPMISC, B_OPBROW, B_OPBLEN, B_OPBPTR,
+        B_OPBCOL, B_OPBVAL, B_OPBCPTR, B_COUNT
     };
     struct Buf {
         void *p = nullptr;
@@ -95,9 +98,27 @@ struct ias_plan {
     ias_status reserve(void **buf, size_t *cap, size_t bytes);
     ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
     // a_entries: stored entries of A (CSR: nnz of the view; ELL: rows * width)
+    ias_status analysis_launch(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
+                               int64_t a_entries);
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                         int64_t cols, int64_t a_entries, ias_report *rep);
     ias::dev::AxView ax_view();
+    // Single pass (csrc/onepass_kernels.hpp): C = A*B into caller arrays of
+    // capacity >= flops(A*B); rows with many products go through the two-phase
+    // engine of `sub` (symbolic before, numeric after the chunk launch).
+    // Sets *nnz_c; order/first_assign as ias::dev::Out.
+    // prepare: analysis, chunking, big-row symbolic (sets flops); run: the
+    // chunk launch + big-row numeric into C of capacity `cap` — when nnz(C)
+    // exceeds it nothing is written beyond, *nnz_c says what is needed and
+    // IAS_ERROR_INSUFFICIENT_CAPACITY is returned (C's row pointer is valid).
+    ias_status onepass_prepare(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
+                               int64_t cols, int64_t a_entries, ias_report *rep);
+    ias_status onepass_run(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t *c_ptr, int32_t *c_col,
+                           double *c_val, int64_t cap, int32_t order, int32_t first_assign, int64_t *nnz_c,
+                           ias_report *rep);
+    ias_plan *sub = nullptr;      // big rows of the single-pass path (two-phase engine)
+    int64_t op_nbig = 0, op_nbe = 0;
+    void *host_info = nullptr;    // pinned scalars of the single-pass path
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
 };

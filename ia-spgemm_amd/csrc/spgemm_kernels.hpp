@@ -54,7 +54,9 @@ struct Timer {
 #if IAS_TIMING
     unsigned long long acc[TIMING_PHASES] = {};
     unsigned long long last = 0;
+    unsigned long long cnt = 0;   // units timed (0: one per flush)
     __device__ __forceinline__ void start() { last = wall_clock64(); }
+    __device__ __forceinline__ void done() { ++cnt; }
     __device__ __forceinline__ void mark(int i) {
         const unsigned long long t = wall_clock64();
         acc[i] += t - last;
@@ -67,10 +69,11 @@ struct Timer {
             g_timing + ((blockIdx.x >> 3) % TIMING_REPS) * (TIMING_SLOTS * (TIMING_PHASES + 1)) +
             slot * (TIMING_PHASES + 1);
         for (int i = 0; i < TIMING_PHASES; ++i) atomicAdd(&g[i], acc[i]);
-        atomicAdd(&g[TIMING_PHASES], 1ull);
+        atomicAdd(&g[TIMING_PHASES], cnt ? cnt : 1ull);
     }
 #else
     __device__ __forceinline__ void start() {}
+    __device__ __forceinline__ void done() {}
     __device__ __forceinline__ void mark(int) {}
     __device__ __forceinline__ void flush(int, bool) {}
 #endif

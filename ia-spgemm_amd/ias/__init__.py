@@ -101,7 +101,7 @@ EXPORTS = [
     "ias_dia_to_csr", "ias_csr_transpose",
     "ias_sizeof_csr", "ias_sizeof_coo", "ias_sizeof_ell", "ias_sizeof_dia",
     "ias_csr_mul_csr", "ias_coo_mul_coo", "ias_ell_mul_ell", "ias_dia_mul_dia",
-    "ias_csr_mul_csr_nnz", "ias_csr_mul_csr_compute",
+    "ias_csr_mul_csr_nnz", "ias_csr_mul_csr_compute", "ias_csr_mul_csr_into",
     "ias_flops", "ias_sum_csr", "ias_sum_coo", "ias_sum_ell", "ias_sum_dia",
     "ias_csr_row_view", "ias_partition_rows", "ias_row_ptr_shift",
     "ias_gen_rmat", "ias_gen_band", "ias_gen_ell",
@@ -152,6 +152,7 @@ def _load():
         "ias_dia_mul_dia": (C.c_int, [P(Dia), P(Dia), P(Dia), P(Opts), P(Report)]),
         "ias_csr_mul_csr_nnz": (C.c_int, [C.c_void_p, P(Csr), P(Csr), i64p, i64p, P(Report)]),
         "ias_csr_mul_csr_compute": (C.c_int, [C.c_void_p, P(Csr), P(Csr), P(Csr), C.c_int32, P(Report)]),
+        "ias_csr_mul_csr_into": (C.c_int, [C.c_void_p, P(Csr), P(Csr), P(Csr), C.c_int32, P(Report)]),
         "ias_flops": (C.c_int, [P(Csr), P(Csr), i64p]),
         "ias_sum_csr": (C.c_int, [P(Csr), f64p]),
         "ias_sum_coo": (C.c_int, [P(Coo), f64p]),

@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define IAS_ABI_VERSION 2   /* 2: ias_report gained ms_stream, stream_products, stream_nnz */
+#define IAS_ABI_VERSION 3   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
+                               3: ias_csr_mul_csr_into (single pass) */
 
 typedef enum ias_status {
     IAS_SUCCESS = 0,
@@ -237,6 +238,21 @@ ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, const ias_csr *
                                int64_t *nnz_c, int64_t *row_ptr_c, ias_report *report);
 ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_csr *B,
                                    ias_csr *C, int32_t order, ias_report *report);
+
+/* Single-call form on device-resident CSR (no separate nnz call).  With
+ * IAS_ONEPASS=1 in the environment it runs the single-pass chunk engine:
+ * symbolic, row pointer and values in one launch over row chunks, the chunk
+ * offsets in C found by a decoupled look-back inside the launch (the fused
+ * form of CSR_MUL_CSR's two loops, csr/common_csr.h:95-189); otherwise the
+ * two-phase engine behind one call.  C->row_ptr
+ * (rows+1), C->col and C->val are caller-provided device arrays of capacity
+ * C->nnz; nnz(C) <= flops(A*B) (ias_flops), so that capacity always suffices.
+ * On success C->nnz = nnz(C).  With less capacity than nnz(C), nothing is
+ * written beyond it, C->row_ptr is complete, C->nnz is set to the nnz needed
+ * and IAS_ERROR_INSUFFICIENT_CAPACITY is returned.  Returns when C is
+ * complete.  order: ias_order. */
+ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, const ias_csr *B, ias_csr *C,
+                                int32_t order, ias_report *report);
 
 /* ---------------------------------------------------------------- verification */
 /* GetFlop (csr/common_csr.h:290-304): sum over stored A(i,j) of nnz(B row j). */

@@ -28,6 +28,14 @@ def need_gpu():
         pytest.fail("no HIP device visible: the gpu tests must run on an MI355X box")
 
 
+@pytest.fixture(params=["onepass", "twophase"], autouse=True)
+def engine(request, monkeypatch):
+    """Every case runs through both CSR engines: the single-pass chunk engine
+    (IAS_ONEPASS=1) and the two-phase engine (the default)."""
+    monkeypatch.setenv("IAS_ONEPASS", "1" if request.param == "onepass" else "0")
+    return request.param
+
+
 def bits(a):
     return np.ascontiguousarray(a, np.float64).view(np.int64)
 
@@ -402,3 +410,96 @@ def test_against_mkl_tolerance():
     absA = ias.HostCsr(A.rows, A.cols, A.row_ptr, A.col, np.abs(A.val))
     bound, _ = ias.spgemm(absA, order=ias.ORDER_SORTED)
     assert np.all(np.abs(got.val - mv) <= 1e-10 * np.maximum(np.abs(mv), bound.val) + 1e-300)
+
+
+# ------------------------------------------------------------------ single pass (ias_csr_mul_csr_into)
+def _dev(A):
+    hs = A.struct()
+    d = ias.Csr()
+    ias.check(ias.lib.ias_csr_copy(C.byref(hs), C.byref(d), ias.MEMORY_DEVICE, 0), "copy")
+    return d
+
+
+def _into(plan, dA, dB, rows, cols, cap, order=ias.ORDER_REFERENCE):
+    dC = ias.Csr()
+    ias.check(ias.lib.ias_csr_alloc(C.byref(dC), rows, cols, cap, ias.MEMORY_DEVICE, 0), "alloc")
+    st = ias.lib.ias_csr_mul_csr_into(plan, C.byref(dA), C.byref(dB), C.byref(dC), order, None)
+    return st, dC
+
+
+def chunk_edges(seed=21):
+    """Rows that stress the chunking of the single pass: > OP_RMAX consecutive
+    empty rows, rows of exactly OP_BIG (2048) and OP_BIG + 1 products, rows of
+    1 product, rows whose product prefix straddles chunk windows, a band block
+    (3-4x compression: most products are duplicates) and an R-MAT block."""
+    rng = np.random.default_rng(seed)
+    n = 20000
+    rows = [[] for _ in range(n)]
+    blen = 16
+    # rows 0..1499 empty (beyond OP_RMAX consecutive)
+    for i in range(1500, 1600):             # exactly 2048 products: 128 entries x 16
+        rows[i] = list(rng.choice(np.arange(12000, n), 128, replace=False))
+    for i in range(1600, 1610):             # 2048 + 16 products: big row path
+        rows[i] = list(rng.choice(np.arange(12000, n), 129, replace=False))
+    for i in range(1610, 1615):             # 6400 products: big row path
+        rows[i] = list(rng.choice(np.arange(12000, n), 400, replace=False))
+    for i in range(1615, 3000):             # 1 entry: 16 products
+        rows[i] = [int(rng.integers(12000, n))]
+    for i in range(3000, 12000):            # band: entries i-3..i+3 -> heavy duplicates
+        rows[i] = [j for j in range(i - 3, i + 4)]
+    for i in range(12000, n):               # 16 random entries (B rows of A = B)
+        rows[i] = list(rng.choice(n, blen, replace=False))
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate([np.asarray(r, np.int64) for r in rows]).astype(np.int32)
+    val = rng.integers(-4, 5, size=col.size).astype(np.float64) + 0.5
+    return ias.HostCsr(n, n, rp, col, val)
+
+
+@pytest.mark.parametrize("which", ["rmat14", "edges", "dups", "long"])
+def test_into_single_call(which, engine):
+    A = {"rmat14": lambda: ias.gen_rmat(14, 16, seed=4), "edges": chunk_edges,
+         "dups": lambda: duplicate_tiers()[0], "long": long_rows}[which]()
+    B = duplicate_tiers()[1] if which == "dups" else A
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    fl = ob.flops(ob.Mat.of(A), ob.Mat.of(B))
+    dA, dB = _dev(A), _dev(B)
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), 0, None), "plan")
+    try:
+        for _ in range(2):   # plan reuse
+            st, dC = _into(plan, dA, dB, A.rows, B.cols, max(fl, 1))
+            ias.check(st, "into")
+            assert dC.nnz == ref.nnz
+            assert_csr_identical(ias.csr_to_numpy(dC), ref, "into " + which)
+        st, dC = _into(plan, dA, dB, A.rows, B.cols, max(fl, 1), ias.ORDER_SORTED)
+        ias.check(st, "into sorted")
+        got = ias.csr_to_numpy(dC)
+        rc, rv = sorted_form(ref)
+        np.testing.assert_array_equal(got.col, rc)
+        np.testing.assert_array_equal(bits(got.val), bits(rv))
+        # too little capacity: row pointer complete, needed nnz reported, nothing written beyond
+        if ref.nnz > 1:
+            st, dC = _into(plan, dA, dB, A.rows, B.cols, ref.nnz - 1)
+            assert st == 11 and dC.nnz == ref.nnz
+            ias.check(ias.lib.ias_csr_free(C.byref(dC)), "free")
+    finally:
+        ias.lib.ias_plan_destroy(plan)
+        ias.lib.ias_csr_free(C.byref(dA))
+        ias.lib.ias_csr_free(C.byref(dB))
+
+
+def test_chunk_edges_all_paths():
+    A = chunk_edges()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, rep = ias.spgemm(A)
+    assert_csr_identical(got, ref, "chunk edges")
+    refc, _ = ob.coo_mul_coo(ob.Mat.of(A), ob.Mat.of(A))
+    ca, cc = _coo_of(A), ias.Coo()
+    o = ias.opts(output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_coo_mul_coo(C.byref(ca), C.byref(ca), C.byref(cc), C.byref(o), None), "coo")
+    n = cc.nnz
+    np.testing.assert_array_equal(ias._np(cc.col, n, np.int32), refc.col)
+    np.testing.assert_array_equal(bits(ias._np(cc.val, n, np.float64)), bits(refc.val))
+    for m in (ca, cc):
+        ias.lib.ias_coo_free(C.byref(m))

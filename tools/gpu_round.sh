@@ -9,7 +9,7 @@ OUT=gpurun_out/${TAG:-run}
 mkdir -p $OUT
 bash tools/probe_box.sh > $OUT/box.txt 2>&1 || true
 make -C ia-spgemm_amd -j16 > $OUT/build.log 2>&1 && make -C oracle >> $OUT/build.log 2>&1 &&
-timeout -k 10 ${TEST_TIMEOUT:-600} python -m pytest tests -m gpu -q ${PYTEST_ARGS:--x} > $OUT/pytest_gpu.log 2>&1 &&
+timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:--x} > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 120 ./ia-spgemm_amd/bin/spgemm-cpu tests/golden/inputs/dia.mtx > $OUT/cli_cpu_dia.txt 2>&1 &&
 timeout -k 10 120 ./ia-spgemm_amd/bin/spgemm-gpu tests/golden/inputs/dia.mtx --aat --rand10 --seed 1 > $OUT/cli_gpu_dia.txt 2>&1 &&

@@ -47,6 +47,8 @@ def main():
             continue
         kind = "symbolic" if slot < 16 else "numeric"
         team = 1 << (slot % 16)
+        if slot >= 30:
+            kind, team = ("onepass" if slot == 31 else "op-big"), 512
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
         print("%-8s TEAM %4d rows %8d  per-row us: %s  sum %.2f" % (
             kind, team, cnt, " ".join("%6.2f" % u for u in us), sum(us)))
