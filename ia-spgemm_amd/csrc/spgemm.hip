@@ -50,131 +50,216 @@ __device__ __forceinline__ int32_t dcap_of(const BinSpec &sp, int b, int32_t k) 
     return sp.dcap[b];
 }
 
-// Block-level count of rows per bin (+ partition items, bitmap words and
-// global-table slots of the rows that need them) into the Counters totals.
+// Block-wide exclusive prefix of a 64-bit value (BLOCK threads); every
+// thread gets the block total.  Two barriers; `red` holds BLOCK/WAVE words.
 template <int BLOCK>
-__device__ __forceinline__ void count_bins(const BinSpec &sp, int b, int32_t k, Counters *cnt) {
-    __shared__ int hist[MAX_BINS];
-    for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK) hist[i] = 0;
+__device__ __forceinline__ unsigned long long block_excl_u64(unsigned long long v, unsigned long long &total,
+                                                             unsigned long long *red) {
+    const int l = (int)(threadIdx.x & (WAVE - 1)), w = (int)(threadIdx.x / WAVE);
+    unsigned long long x = v;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const unsigned long long t = __shfl_up(x, d);
+        if (l >= d) x += t;
+    }
+    if (l == WAVE - 1) red[w] = x;
     __syncthreads();
-    if (b > 0) {
-        atomicAdd(&hist[b], 1);
-        if (sp.ft) atomicAdd(&cnt->bm_words, (unsigned long long)((k + 31) / 32));
-        const int32_t dc = dcap_of(sp, b, k);
-        if (dc > 0) atomicAdd(&cnt->dup_slots, (unsigned long long)dc);
-        if (b == sp.nval + 1) {
-            atomicAdd(&cnt->items, (unsigned long long)nparts_of(k, sp.part_cap));
-        } else if (b == sp.nval + 2) {
-            const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
-            unsigned long long S = 1;
-            while (S < need) S <<= 1;
-            atomicAdd(&cnt->ws_slots, S);
-        }
+    unsigned long long before = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < BLOCK / WAVE; ++i) {
+        before += i < w ? red[i] : 0ull;
+        tot += red[i];
     }
     __syncthreads();
+    total = tot;
+    return before + x - v;
+}
+
+// Per-row allocation sizes of a binned row: bitmap words, duplicate slots,
+// partition items, global-table slots.
+__device__ __forceinline__ void bin_needs(const BinSpec &sp, int b, int32_t k, unsigned long long (&q)[4]) {
+    q[0] = q[1] = q[2] = q[3] = 0ull;
+    if (b <= 0) return;
+    if (sp.ft) q[0] = (unsigned long long)((k + 31) / 32);
+    const int32_t dc = dcap_of(sp, b, k);
+    if (dc > 0) q[1] = (unsigned long long)dc;
+    if (b == sp.nval + 1) {
+        q[2] = (unsigned long long)nparts_of(k, sp.part_cap);
+    } else if (b == sp.nval + 2) {
+        const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
+        unsigned long long S = 1;
+        while (S < need) S <<= 1;
+        q[3] = S;
+    }
+}
+
+// Block-level count of rows per bin (+ the allocation totals) into the
+// Counters, R rows per thread: one global atomic per block and counter.  The
+// counters share a few cache lines, so atomics on them serialise: blocks of
+// BLOCK*R rows keep their number small.
+template <int BLOCK, int R>
+__device__ __forceinline__ void count_bins(const BinSpec &sp, const int (&b)[R], const int32_t (&k)[R],
+                                           Counters *cnt) {
+    __shared__ int hist[MAX_BINS];
+    __shared__ unsigned long long red[4][BLOCK / WAVE];
+    for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK) hist[i] = 0;
+    __syncthreads();
+    unsigned long long q[4] = {0ull, 0ull, 0ull, 0ull};   // bm_words, dup_slots, items, ws_slots
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        if (b[i] > 0) {
+            atomicAdd(&hist[b[i]], 1);
+            unsigned long long n[4];
+            bin_needs(sp, b[i], k[i], n);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q[j] += n[j];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int d = WAVE / 2; d > 0; d >>= 1) q[j] += __shfl_xor(q[j], d);
+    if ((threadIdx.x & (WAVE - 1)) == 0)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[j][threadIdx.x / WAVE] = q[j];
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int i = 0; i < BLOCK / WAVE; ++i) t += red[threadIdx.x][i];
+        unsigned long long *dst[4] = {&cnt->bm_words, &cnt->dup_slots, &cnt->items, &cnt->ws_slots};
+        if (t) atomicAdd(dst[threadIdx.x], t);
+    }
     for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK)
         if (i > 0 && hist[i] > 0) atomicAdd(&cnt->count[i], hist[i]);
 }
 
 // ---------------------------------------------------------------- analysis
-// Products per row (GetFlop per row) and the expanded A (AxView).  A block
-// owns 256 consecutive rows and spreads their A entries over its threads (a
-// hub row does not serialise on one lane).  Also accumulates total flops, the
-// max products per row, and the symbolic bin counts.
+// Three passes, all load-balanced: the row of every stored A entry (CSR:
+// AN_FILL lanes per row), then flat over A entries the expanded A (B-row start and
+// length, A value) — independent of how entries spread over rows, so R-MAT
+// hub rows do not serialise a block — and, after the scan of the B-row
+// lengths, per row: products (GetFlop per row, csr/common_csr.h:290-304) =
+// difference of the product offsets, the symbolic bin counts, total flops
+// and the max products per row.
 constexpr int AN_BLOCK = 256;
+constexpr int AN_U = 4;   // entries per thread in flight
 
-__global__ __launch_bounds__(AN_BLOCK) void k_row_products(Rows A, Rows B, int64_t rows, AxOut ax,
-                                                           int64_t a_entries, int32_t *prod,
-                                                           BinSpec spec, Counters *cnt) {
-    __shared__ int64_t start[AN_BLOCK];
-    __shared__ int32_t pref[AN_BLOCK + 1];
-    __shared__ unsigned long long acc[AN_BLOCK];
-    __shared__ int scratch[8];
-    const int t = threadIdx.x;
-    const int64_t r = (int64_t)blockIdx.x * AN_BLOCK + t;
+constexpr int AN_FILL = 16;   // lanes per row of k_an_rowfill
+__global__ void k_an_rowfill(Rows A, int64_t rows, int64_t a_entries, int32_t *axr, Counters *cnt) {
+    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / AN_FILL;
+    const int lane = threadIdx.x & (AN_FILL - 1);
+    if (r >= rows) return;
+    int64_t s;
+    int32_t n;
+    A.row(r, s, n);
+    const int64_t q0 = s - A.base();
+    if (q0 < 0 || q0 + n > a_entries) {
+        if (lane == 0) cnt->overflow = 1;   // row pointer disagrees with the declared entry count
+        return;
+    }
+    for (int32_t i = lane; i < n; i += AN_FILL) axr[q0 + i] = (int32_t)r;
+}
+
+// Expanded A, flat over entries.  CSR: rows from k_an_rowfill; ELL (A.ptr
+// null): row = q / stride, padding entries (beyond len[row]) get no products.
+__global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t a_entries, AxOut ax) {
     const int64_t abase = A.base();
-    int64_t s = 0;
-    int32_t n = 0;
-    if (r < rows) A.row(r, s, n);
-    start[t] = s;
-    acc[t] = 0;
-    {
-        int tot;
-        const int ex = Team<AN_BLOCK>::excl_sum(n, tot, scratch);
-        pref[t] = ex;
-        if (t == 0) pref[AN_BLOCK] = tot;
-    }
-    __syncthreads();
-    const int32_t E = pref[AN_BLOCK];
-    for (int32_t e = t; e < E; e += AN_BLOCK) {
-        const int lo = seg_find(pref, AN_BLOCK, e);
-        const int64_t ea = start[lo] + (e - pref[lo]);
-        const int32_t j = A.col[ea];
-        int64_t bs;
-        int32_t bn;
-        B.row(j, bs, bn);
-        const int64_t q = ea - abase;
-        if (q >= 0 && q < a_entries) {
-            ax.row[q] = (int32_t)((int64_t)blockIdx.x * AN_BLOCK + lo);
-            ax.bstart[q] = bs;
-            ax.blen[q] = bn;
-            ax.aval[q] = A.val[ea];
-        } else {
-            cnt->overflow = 1;   // row pointer disagrees with the declared entry count
+    const int64_t step = (int64_t)gridDim.x * AN_BLOCK * AN_U;
+    for (int64_t q0 = (int64_t)blockIdx.x * AN_BLOCK * AN_U + threadIdx.x; q0 < a_entries; q0 += step) {
+        int32_t j[AN_U], bn[AN_U];
+        int64_t bs[AN_U];
+        double av[AN_U];
+        bool ok[AN_U];
+#pragma unroll
+        for (int u = 0; u < AN_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * AN_BLOCK;
+            ok[u] = q < a_entries;
+            if (ok[u] && !A.ptr) ok[u] = (q % A.stride) < A.len[q / A.stride];
+            j[u] = ok[u] ? A.col[abase + q] : 0;
         }
-        atomicAdd(&acc[lo], (unsigned long long)bn);
-    }
-    __syncthreads();
-    const unsigned long long mine = acc[t];
-    const int mx0 = (int)min(mine, (unsigned long long)INT32_MAX);
-    if (r < rows) prod[r] = mx0;
-    count_bins<AN_BLOCK>(spec, r < rows ? bin_of(spec, mx0, mx0, -2) : -1, mx0, cnt);
-    __shared__ unsigned long long red_sum[AN_BLOCK / WAVE];
-    __shared__ int red_max[AN_BLOCK / WAVE];
-    unsigned long long sm = (r < rows) ? mine : 0ull;
-    int mx = (r < rows) ? mx0 : 0;
-    for (int d = WAVE / 2; d > 0; d >>= 1) {
-        sm += __shfl_down(sm, d);
-        mx = max(mx, __shfl_down(mx, d));
-    }
-    if ((t & (WAVE - 1)) == 0) {
-        red_sum[t / WAVE] = sm;
-        red_max[t / WAVE] = mx;
-    }
-    __syncthreads();
-    if (t == 0) {
-        unsigned long long S = 0;
-        int MX = 0;
-        for (int i = 0; i < AN_BLOCK / WAVE; ++i) {
-            S += red_sum[i];
-            MX = max(MX, red_max[i]);
+#pragma unroll
+        for (int u = 0; u < AN_U; ++u) {   // all loads before any store (no alias ordering)
+            bn[u] = 0;
+            bs[u] = 0;
+            av[u] = 0.0;
+            if (ok[u]) {
+                B.row(j[u], bs[u], bn[u]);
+                av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
+            }
         }
-        atomicAdd(&cnt->flops, S);
-        atomicMax(&cnt->max_prod, MX);
+#pragma unroll
+        for (int u = 0; u < AN_U; ++u) {
+            const int64_t q = q0 + (int64_t)u * AN_BLOCK;
+            if (q >= a_entries) continue;
+            ax.bstart[q] = bs[u];
+            ax.blen[q] = bn[u];
+            ax.aval[q] = av[u];
+            if (!A.ptr) ax.row[q] = (int32_t)(q / A.stride);
+        }
     }
 }
 
 constexpr int BIN_BLOCK = 256;
+constexpr int BIN_RPT = 8;                       // rows per thread of the row passes
+constexpr int BIN_ROWS = BIN_BLOCK * BIN_RPT;    // rows per block
+
+__global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int64_t rows, int32_t *prod,
+                                                       BinSpec spec, Counters *cnt) {
+    int b[BIN_RPT];
+    int32_t k[BIN_RPT];
+    int mx = 0;
+#pragma unroll
+    for (int i = 0; i < BIN_RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + threadIdx.x;
+        b[i] = -1;
+        k[i] = 0;
+        if (r < rows) {
+            const int64_t p = poff[r + 1] - poff[r];
+            k[i] = (int32_t)min(p, (int64_t)INT32_MAX);
+            prod[r] = k[i];
+            b[i] = bin_of(spec, k[i], k[i], -2);
+            mx = max(mx, k[i]);
+        }
+    }
+    count_bins<BIN_BLOCK, BIN_RPT>(spec, b, k, cnt);
+#pragma unroll
+    for (int d = WAVE / 2; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d));
+    __shared__ int wmx[BIN_BLOCK / WAVE];
+    if ((threadIdx.x & (WAVE - 1)) == 0) wmx[threadIdx.x / WAVE] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < BIN_BLOCK / WAVE; ++i) mx = max(mx, wmx[i]);
+        if (mx > 0) atomicMax(&cnt->max_prod, mx);
+        if (blockIdx.x == 0) cnt->flops = (unsigned long long)(poff[rows] - poff[0]);
+    }
+}
 
 // Counting pass of a binning (numeric and sort binnings; the symbolic one is
-// fused into k_row_products).  prod may be null (class test off); a row is
+// fused into k_an_rows).  prod may be null (class test off); a row is
 // streaming-class when stn is given and stn[r] >= 0.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, const int32_t *prod,
                                                          const int32_t *stn, int64_t rows,
                                                          BinSpec spec, Counters *cnt) {
-    const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + threadIdx.x;
-    int b = -1;
-    int32_t k = 0;
+    int b[BIN_RPT];
+    int32_t k[BIN_RPT];
     unsigned long long sp = 0, sn = 0;
-    if (r < rows) {
-        k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k, stn ? stn[r] : -2);
-        if (stn && stn[r] >= 0 && k > 0) {   // a streaming row: its work in the flat pass
-            sp = (unsigned long long)(prod ? prod[r] : k);
-            sn = (unsigned long long)k;
+#pragma unroll
+    for (int i = 0; i < BIN_RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + threadIdx.x;
+        b[i] = -1;
+        k[i] = 0;
+        if (r < rows) {
+            k[i] = key[r];
+            const int32_t st = stn ? stn[r] : -2;
+            const int32_t pr = prod ? prod[r] : k[i];
+            b[i] = bin_of(spec, k[i], pr, st);
+            if (stn && st >= 0 && k[i] > 0) {   // a streaming row: its work in the flat pass
+                sp += (unsigned long long)pr;
+                sn += (unsigned long long)k[i];
+            }
         }
     }
-    count_bins<BIN_BLOCK>(spec, b, k, cnt);
+    count_bins<BIN_BLOCK, BIN_RPT>(spec, b, k, cnt);
     if (stn) {   // block sums, one pair of atomics per block
         __shared__ unsigned long long red[2][BIN_BLOCK / WAVE];
         for (int d = WAVE / 2; d > 0; d >>= 1) {
@@ -204,6 +289,8 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
 // (bins laid out in bin order, offsets = prefix of the counted totals);
 // partitioned rows get one PartItem per partition (+ a bitmap offset when
 // FT); global-table rows a workspace offset of nextpow2(ceil(k*3/2)) slots.
+// R rows per thread; per-row allocations come from a block prefix and one
+// cursor atomic per block and counter.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, const int32_t *prod,
                                                            const int32_t *stn, int64_t rows,
                                                            BinSpec spec, Rows A, RowRef *lists,
@@ -214,6 +301,8 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     __shared__ int hist[MAX_BINS];
     __shared__ int64_t base[MAX_BINS];
     __shared__ int64_t bin_start[MAX_BINS];
+    __shared__ unsigned long long red[BIN_BLOCK / WAVE];
+    __shared__ unsigned long long cbase[4];
     const int t = threadIdx.x;
     if (t < MAX_BINS) hist[t] = 0;
     if (t == 0) {
@@ -224,51 +313,73 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         }
     }
     __syncthreads();
-    const int64_t r = (int64_t)blockIdx.x * BIN_BLOCK + t;
     const int part_bin = spec.nval + 1, wide_bin = spec.nval + 2;
-    int b = -1, local = 0;
-    int32_t k = 0;
-    if (r < rows) {
-        k = key[r];
-        b = bin_of(spec, k, prod ? prod[r] : k, stn ? stn[r] : -2);
-        if (b == 0 && spec.zero_nnz) nnz_row[r] = 0;
-        if (b == 0 && dupn) dupn[r] = 0;
-        if (b > 0) local = atomicAdd(&hist[b], 1);
+    int b[BIN_RPT], local[BIN_RPT];
+    int32_t k[BIN_RPT];
+    unsigned long long mine[4] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+    for (int i = 0; i < BIN_RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
+        b[i] = -1;
+        local[i] = 0;
+        k[i] = 0;
+        if (r < rows) {
+            k[i] = key[r];
+            b[i] = bin_of(spec, k[i], prod ? prod[r] : k[i], stn ? stn[r] : -2);
+            if (b[i] == 0 && spec.zero_nnz) nnz_row[r] = 0;
+            if (b[i] == 0 && dupn) dupn[r] = 0;
+            if (b[i] > 0) local[i] = atomicAdd(&hist[b[i]], 1);
+            unsigned long long n[4];
+            bin_needs(spec, b[i], k[i], n);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) mine[j] += n[j];
+        }
     }
     __syncthreads();
     if (t > 0 && t < MAX_BINS && hist[t] > 0) base[t] = atomicAdd(&cnt->cursor[t], hist[t]);
+    unsigned long long at[4], tot[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) at[j] = block_excl_u64<BIN_BLOCK>(mine[j], tot[j], red);
+    if (t < 4) {
+        unsigned long long *cur[4] = {&cnt->bm_cur, &cnt->dup_cur, &cnt->items_cur, &cnt->ws_cur};
+        cbase[t] = tot[t] ? atomicAdd(cur[t], tot[t]) : 0ull;
+    }
     __syncthreads();
-    if (b > 0) {
-        const int64_t within = base[b] + local;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) at[j] += cbase[j];
+#pragma unroll
+    for (int i = 0; i < BIN_RPT; ++i) {
+        if (b[i] <= 0) continue;
+        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
+        unsigned long long n[4];
+        bin_needs(spec, b[i], k[i], n);
+        const int64_t within = base[b[i]] + local[i];
         RowRef ref;
         ref.row = (int32_t)r;
         if (qstart) {   // products of the row in the expansion
             ref.q0 = qstart[r];
-            ref.n = k;
+            ref.n = k[i];
         } else {        // entries of the row in the expanded A
             int64_t s;
-            int32_t n;
-            A.row(r, s, n);
+            int32_t nn;
+            A.row(r, s, nn);
             ref.q0 = s - A.base();
-            ref.n = n;
+            ref.n = nn;
         }
-        lists[bin_start[b] + within] = ref;
-        if (spec.ft) bm_off[r] = (int64_t)atomicAdd(&cnt->bm_cur, (unsigned long long)((k + 31) / 32));
-        const int32_t dc = dcap_of(spec, b, k);
-        if (dc > 0) dup_off[r] = (int64_t)atomicAdd(&cnt->dup_cur, (unsigned long long)dc);
-        if (b == part_bin) {
-            const uint32_t np = nparts_of(k, spec.part_cap);
-            const unsigned long long at = atomicAdd(&cnt->items_cur, (unsigned long long)np);
-            for (uint32_t q = 0; q < np; ++q) items[at + q] = PartItem{ref, q, np};
+        lists[bin_start[b[i]] + within] = ref;
+        if (spec.ft) bm_off[r] = (int64_t)at[0];
+        if (n[1]) dup_off[r] = (int64_t)at[1];
+        if (b[i] == part_bin) {
+            const uint32_t np = (uint32_t)n[2];
+            for (uint32_t q = 0; q < np; ++q) items[at[2] + q] = PartItem{ref, q, np};
             if (spec.zero_nnz) nnz_row[r] = 0;
             // partitioned rows: a duplicate counter (k_dup_place decides the path)
             if (dupn) dupn[r] = spec.part_dcap_div > 0 ? 0 : -1;
-        } else if (b == wide_bin) {
-            const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
-            unsigned long long S = 1;
-            while (S < need) S <<= 1;
-            ws_off[within] = (int64_t)atomicAdd(&cnt->ws_cur, S);
+        } else if (b[i] == wide_bin) {
+            ws_off[within] = (int64_t)at[3];
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) at[j] += n[j];
     }
 }
 
@@ -1366,15 +1477,15 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     int32_t *axr = as<int32_t>(bufs[B_AXR]);
     int64_t *axp = as<int64_t>(bufs[B_AXP]);
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
-    if (!A.ptr && a_entries > 0) {   // ELL padding entries: no products, any valid row
-        HIPC(hipMemsetAsync(axl, 0, sizeof(int32_t) * a_entries, s));
-        HIPC(hipMemsetAsync(axr, 0, sizeof(int32_t) * a_entries, s));
+    if (A.ptr && rows > 0)
+        k_an_rowfill<<<grid_for(rows * AN_FILL, 256), 256, 0, s>>>(A, rows, a_entries, axr, dc);
+    if (a_entries > 0) {
+        const int64_t per = (int64_t)AN_BLOCK * AN_U;
+        const unsigned g = (unsigned)std::min<int64_t>((a_entries + per - 1) / per, 16384);
+        k_an_entries<<<g, AN_BLOCK, 0, s>>>(A, B, a_entries,
+                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, as<double>(bufs[B_AXV]), axr});
     }
-    if (rows > 0)
-        k_row_products<<<grid_for(rows, AN_BLOCK), AN_BLOCK, 0, s>>>(
-            A, B, rows, AxOut{as<int64_t>(bufs[B_AXS]), axl, as<double>(bufs[B_AXV]), axr},
-            a_entries, as<int32_t>(bufs[B_PROD]), ss, dc);
-    CHECK_LAUNCH("k_row_products", s);
+    CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
         k_scan_reduce<<<(unsigned)nbe, SCAN_BLOCK, 0, s>>>(axl, a_entries, as<int64_t>(bufs[B_PART2]), nullptr);
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART2]), nbe);
@@ -1383,6 +1494,8 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
         HIPC(hipMemsetAsync(axp, 0, sizeof(int64_t), s));
     }
     k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff);
+    if (rows > 0)
+        k_an_rows<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc);
     CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
@@ -1436,7 +1549,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     RowRef *SL = as<RowRef>(bufs[B_SLIST]);
     int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
     if (rows > 0)
-        k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
+        k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
             as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc);
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
@@ -1476,9 +1589,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART]), nb);
         k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
     CHECK_LAUNCH("scan", s);
-        k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
+        k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
                                                                     rows, ns, dc2);
-        k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(
+        k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
             nullptr, dc2);
@@ -1828,8 +1941,8 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
     // the scatter's row extents are not used by the sort kernels (they read ptr/len)
     const Rows span{ptr, len, stride, nullptr, nullptr};
-    k_bin_count<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
-    k_bin_scatter<<<grid_for(rows, BIN_BLOCK), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
+    k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
+    k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
                                                                   lists, nullptr, nullptr, offs, nullptr,
                                                                   nullptr, nullptr, nullptr, dc);
     Counters hc;

@@ -794,6 +794,11 @@ struct FlatEntry {
 constexpr int FLAT_MW = 64;
 
 template <int K>
+// FLAT_BCOL=1: the flat numeric reads the product's column from B itself
+// (the line it gathers the value's row from) instead of the expansion.
+#ifndef FLAT_BCOL
+#define FLAT_BCOL 0
+#endif
 __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows &B, const FlatArgs &fa,
                                                    const Out &out, int64_t q0, FlatEntry *ent,
                                                    unsigned long long *masks) {
@@ -868,7 +873,11 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
                         const FlatEntry &E = ent[ei];
                         S.ei[k] = ei;
                         S.j[k] = t - E.start;
+#if FLAT_BCOL
+                        S.c[k] = B.col[E.bstart + S.j[k]];   // beside the value: same B row
+#else
                         S.c[k] = fa.tcol[E.g + S.j[k]];
+#endif
                         S.bv[k] = B.val[E.bstart + S.j[k]];
                         const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
                         S.word[k] = fa.bm.bits[E.bmw + (p >> 5)];
