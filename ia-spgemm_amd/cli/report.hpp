@@ -8,6 +8,7 @@
 #include <sys/time.h>
 
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -82,13 +83,51 @@ inline int report(const std::vector<AlgResult> &r, long long flops, bool speedup
     return best_i;
 }
 
-// Format selector (the "input-aware" choice).  MatNet needs
-// Keras, which is not available; this deterministic rule uses the same
-// feature families (GetInfo1 row statistics, GetInfo2 DIA fill, GetInfo3 ELL
-// fill): banded -> DIA, uniform rows -> ELL, else the CSR hash path.
-// Returns a 0-based algorithm index into {MKL, CSR, DIA, ELL, COO}.
-inline int select_format(const ias_csr &A, bool dia_ok, double dia_fill, bool ell_ok, double ell_fill) {
-    (void)A;
+// Python's repr of a float (MatNet.py:27 prints the features as a list).
+inline std::string py_float(double v) {
+    char buf[64];
+    auto r = std::to_chars(buf, buf + sizeof buf, v);
+    std::string s(buf, r.ptr);
+    if (s.find_first_of(".en") == std::string::npos) s += ".0";
+    return s;
+}
+
+// The input-aware choice (main.cpp:651-704, GPU/main.cu:434-460):
+// features + density images of A and B into MatNet with the reference's own
+// weights (libias: ias_features, ias_density_image, ias_matnet_*).  Prints
+// MatNet.py's "matrix features" and "Prediction cost" lines.  $IAS_MATNET
+// overrides the weight set (a name or a blob path).  Returns the 0-based
+// class, or `fallback` when the weights cannot be loaded.
+inline int matnet_choose(const ias_csr &A, const ias_csr &B, int nfeatures, const char *weights, int fallback) {
+    const char *env = getenv("IAS_MATNET");
+    if (env && *env) weights = env;
+    std::vector<double> f((size_t)nfeatures);
+    std::vector<int64_t> ia(IAS_IMAGE_SIDE * IAS_IMAGE_SIDE), ib(IAS_IMAGE_SIDE * IAS_IMAGE_SIDE);
+    CLI_TRY("features", ias_features(&A, &B, nfeatures, f.data()));
+    CLI_TRY("image", ias_density_image(&A, ia.data()));
+    CLI_TRY("image", ias_density_image(&B, ib.data()));
+    printf("matrix features: [");
+    for (int i = 0; i < nfeatures; ++i) printf("%s%s", i ? ", " : "", py_float(f[i]).c_str());
+    printf("]\n");
+    ias_matnet *net = nullptr;
+    ias_status s = ias_matnet_load(weights, &net);
+    if (s != IAS_SUCCESS) {
+        printf("MatNet weights unavailable (%s): fallback choice\n", ias_last_error());
+        return fallback;
+    }
+    int32_t nf = 0, chosen = fallback;
+    ias_matnet_shape(net, &nf, nullptr);
+    const double t = now_ms();
+    if (nf == nfeatures) CLI_TRY("matnet", ias_matnet_predict(net, ia.data(), ib.data(), f.data(), nullptr, &chosen));
+    printf("Prediction cost: %f seconds\n", (now_ms() - t) / 1000.0);
+    ias_matnet_free(net);
+    return chosen;
+}
+
+// Deterministic fallback when no weights are available: banded -> DIA,
+// uniform rows -> ELL, else the CSR hash path (0-based into {MKL, CSR, DIA,
+// ELL, COO}).
+inline int select_format(bool dia_ok, double dia_fill, bool ell_ok, double ell_fill) {
     if (dia_ok && dia_fill >= 0.5) return 2;
     if (ell_ok && ell_fill >= 0.9) return 3;
     return 1;

@@ -5,9 +5,10 @@
 // Usage: spgemm-cpu A.mtx [B.mtx] [testing_mode 0|1] [--no-warmup]
 //   B defaults to A (C = A*A, the README's intent; the reference's own
 //   argv[3] read before the argc check is undefined behaviour, main.cpp:99).
-// Differences from the reference, all documented in INTEGRATION.md: no
-// embedded CPython/MatNet (a deterministic selector prints "The Chosen One");
-// no pthread timeout cancellation; trans_time prints the measured conversion
+// "The Chosen One" comes from MatNet run natively (libias: the reference's
+// Intel weights, exported from NetWeights/Intel_weights.h5) instead of
+// embedded CPython/Keras.  Other differences, documented in INTEGRATION.md: no
+// pthread timeout cancellation; trans_time prints the measured conversion
 // time of the format (the reference prints uninitialised slots).
 #include "ias.h"
 #include "report.hpp"
@@ -63,7 +64,7 @@ int main(int argc, char **argv) {
     }
     std::printf("------------------------------------------\n");
 
-    // ---- formats + selector (features: GetInfo2 / GetInfo3 families)
+    // ---- formats + selector (MatNet over GetInfo1/2/3 features and density images)
     ias_dia Ad{}, Bd{};
     ias_ell Ae{}, Be{};
     ias_coo Ac{}, Bc{};
@@ -84,7 +85,8 @@ int main(int argc, char **argv) {
     const bool coo_ok = ell_ok && sc == IAS_SUCCESS && sc2 == IAS_SUCCESS;   // main.cpp:917 gates COO on ELL
     const double dia_fill = Ad.num_diagonals ? (double)A.nnz / ((double)Ad.num_diagonals * A.rows) : 0.0;
     const double ell_fill = Ae.max_nnz_per_row ? (double)A.nnz / ((double)Ae.max_nnz_per_row * A.rows) : 0.0;
-    const int chosen = cli::select_format(A, dia_ok, dia_fill, ell_ok, ell_fill);
+    const int chosen = cli::matnet_choose(A, B, 26, "intel",
+                                          cli::select_format(dia_ok, dia_fill, ell_ok, ell_fill));
     std::printf("The Chosen One = Algorithm %d\n", chosen + 1);
 
     std::vector<AlgResult> r(5);

@@ -1,5 +1,6 @@
 // spgemm-gpu — drop-in for IA-SPGEMM-GPU_release/main.cu (the `spgemm-gpu`
-// program).  Reads one .mtx and reports the GPU algorithms; the reference's
+// program).  Reads one .mtx, asks MatNet (the reference's P100 weights, run
+// natively) for its choice, and reports the GPU algorithms; the reference's
 // Algorithm 1 (CUSP ESC, main.cu:467-505) and Algorithm 2 (cuSPARSE csrgemm,
 // main.cu:508-523) are replaced by this engine's two output orders:
 //   1 IAS row-wise hash, reference order (byte-identical to CSR_MUL_CSR)
@@ -42,13 +43,10 @@ int main(int argc, char **argv) {
     int64_t flops = 0;
     CLI_TRY("flops", ias_flops(&A, &B, &flops));
 
-    const bool ell_ok = true;
-    ias_ell Ae{};
-    double ell_fill = 0;
-    if (ias_csr_to_ell(&A, &Ae, 20.0) == IAS_SUCCESS)
-        ell_fill = Ae.max_nnz_per_row ? (double)A.nnz / ((double)Ae.max_nnz_per_row * A.rows) : 0;
-    ias_ell_free(&Ae);
-    const int chosen = cli::select_format(A, false, 0.0, ell_ok, ell_fill) == 1 ? 0 : 1;
+    // MatNet with the reference's P100 weights over GetInfo1(A), GetInfo1(B)
+    // and the two density images (GPU/main.cu:276-460); classes {CUSP,
+    // cuSPARSE, NSPARSE}; without weights the hash path (class 1) is assumed.
+    const int chosen = cli::matnet_choose(A, B, 18, "p100", 1);
     std::printf("The Chosen One = Algorithm %d\n", chosen + 1);
 
     ias_csr dA{}, dB{};
@@ -75,7 +73,8 @@ int main(int argc, char **argv) {
     }
     ias_plan_destroy(o.plan);
     cli::report(r, (long long)flops, false, false);
-    std::printf("MatNet predicts Algorithm %s is optimal\n", chosen == 0 ? "IAS-hash" : "IAS-sorted");
+    static const char *names[3] = {"CUSP", "cuSPARSE", "NSPARSE"};   // GPU/main.cu:539-544
+    if (chosen >= 0 && chosen < 3) std::printf("MatNet predicts Algorithm %s is optimal\n", names[chosen]);
     ias_csr_free(&dA); ias_csr_free(&dB);
     ias_csr_free(&A); ias_csr_free(&B);
     return 0;

@@ -815,7 +815,13 @@ __global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t 
                 if (w0 + EK < nwin) load(w0 + EK, cn, tn);
 #pragma unroll
                 for (int k = 0; k < EK; ++k)
-                    if (tt[k] >= 0) tcol[G0 + tt[k]] = c[k];
+                    if (tt[k] >= 0) {
+#if STREAM_NT
+                        __builtin_nontemporal_store(c[k], &tcol[G0 + tt[k]]);
+#else
+                        tcol[G0 + tt[k]] = c[k];
+#endif
+                    }
 #pragma unroll
                 for (int k = 0; k < EK; ++k) {
                     c[k] = cn[k];

@@ -38,6 +38,17 @@ constexpr int32_t EMPTY_KEY = -1;
 #ifndef IAS_ABLATE
 #define IAS_ABLATE 0
 #endif
+#ifndef STREAM_NT
+#define STREAM_NT 1
+#endif
+// a read of the expansion (tcol): streamed once per pass
+__device__ __forceinline__ int32_t ld_stream(const int32_t *p) {
+#if STREAM_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
 
 // Timing-only builds (-DIAS_TIMING=1, tools/timing.sh; never shipped): per-
 // phase wall-clock cycles of the row kernels, summed per (kind, log2 TEAM)
@@ -601,7 +612,7 @@ __device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const 
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int p = p0 + k * TEAM + lane;
-            c[k] = p < P ? pc[p] : EMPTY_KEY;
+            c[k] = p < P ? ld_stream(pc + p) : EMPTY_KEY;
             pp[k] = (uint32_t)p;
         }
 #pragma unroll
@@ -654,7 +665,7 @@ __device__ __forceinline__ void load_step(const int32_t *tcol, const RowRef &ref
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int p = p0 + k * TEAM + lane;
-        c[k] = p < ref.n ? pc[p] : EMPTY_KEY;
+        c[k] = p < ref.n ? ld_stream(pc + p) : EMPTY_KEY;
     }
 }
 
@@ -799,6 +810,11 @@ template <int K>
 #ifndef FLAT_BCOL
 #define FLAT_BCOL 0
 #endif
+// FLAT_NT=1: C leaves through non-temporal stores (not read back; B's rows
+// keep the caches); STREAM_NT=1: the expansion is written and read the same way.
+#ifndef FLAT_NT
+#define FLAT_NT 1
+#endif
 __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows &B, const FlatArgs &fa,
                                                    const Out &out, int64_t q0, FlatEntry *ent,
                                                    unsigned long long *masks) {
@@ -876,7 +892,7 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
 #if FLAT_BCOL
                         S.c[k] = B.col[E.bstart + S.j[k]];   // beside the value: same B row
 #else
-                        S.c[k] = fa.tcol[E.g + S.j[k]];
+                        S.c[k] = ld_stream(fa.tcol + E.g + S.j[k]);
 #endif
                         S.bv[k] = B.val[E.bstart + S.j[k]];
                         const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
@@ -899,8 +915,13 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
                 const uint32_t rk = cur.pre[k] + (uint32_t)__popc(cur.word[k] & ((1u << (p & 31)) - 1u));
                 if ((cur.word[k] >> (p & 31)) & 1u) {
                     const int64_t pos = E.cbase + sgn * (int64_t)rk;
+#if FLAT_NT
+                    __builtin_nontemporal_store(cur.c[k], &out.col[pos]);
+                    __builtin_nontemporal_store(out.first_assign ? prod : 0.0 + prod, &out.val[pos]);
+#else
                     out.col[pos] = cur.c[k];
                     out.val[pos] = out.first_assign ? prod : 0.0 + prod;
+#endif
                 } else {
                     fa.dupval[E.dbase + (p - rk)] = prod;
                 }

@@ -106,6 +106,8 @@ EXPORTS = [
     "ias_csr_row_view", "ias_partition_rows", "ias_row_ptr_shift",
     "ias_gen_rmat", "ias_gen_band", "ias_gen_ell",
     "ias_mkl_available", "ias_mkl_sp2m",
+    "ias_features", "ias_density_image", "ias_matnet_load", "ias_matnet_free", "ias_matnet_shape",
+    "ias_matnet_predict",
 ]
 
 
@@ -167,6 +169,12 @@ def _load():
         "ias_gen_ell": (C.c_int, [C.c_int64, C.c_int32, C.c_uint64, C.c_int32, P(Csr)]),
         "ias_mkl_available": (C.c_int, [i32p, C.c_char_p, C.c_int32]),
         "ias_mkl_sp2m": (C.c_int, [P(Csr), P(Csr), P(Csr), C.c_int32, f64p]),
+        "ias_features": (C.c_int, [P(Csr), P(Csr), C.c_int32, f64p]),
+        "ias_density_image": (C.c_int, [P(Csr), i64p]),
+        "ias_matnet_load": (C.c_int, [C.c_char_p, P(C.c_void_p)]),
+        "ias_matnet_free": (C.c_int, [C.c_void_p]),
+        "ias_matnet_shape": (C.c_int, [C.c_void_p, i32p, i32p]),
+        "ias_matnet_predict": (C.c_int, [C.c_void_p, i64p, i64p, f64p, C.POINTER(C.c_float), i32p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -326,3 +334,38 @@ def mkl_sp2m(A: HostCsr, B: HostCsr, threads=0):
     ms = C.c_double(0)
     check(lib.ias_mkl_sp2m(C.byref(sa), C.byref(sb), C.byref(c), threads, C.byref(ms)), "ias_mkl_sp2m")
     return csr_to_numpy(c), float(ms.value)
+
+
+# ---------------------------------------------------------------- input-aware selector
+def features(A: HostCsr, B: HostCsr, n: int = 26) -> np.ndarray:
+    sa, sb = A.struct(), B.struct()
+    out = np.zeros(n, np.float64)
+    check(lib.ias_features(C.byref(sa), C.byref(sb), n, _ptr(out, C.c_double)), "ias_features")
+    return out
+
+
+def density_image(A: HostCsr) -> np.ndarray:
+    sa = A.struct()
+    out = np.zeros(128 * 128, np.int64)
+    check(lib.ias_density_image(C.byref(sa), _ptr(out, C.c_int64)), "ias_density_image")
+    return out.reshape(128, 128)
+
+
+def matnet_predict(weights: str, img_a: np.ndarray, img_b: np.ndarray, feats: np.ndarray):
+    """(chosen, probs) of MatNet with the named weight set (or blob path)."""
+    net = C.c_void_p()
+    check(lib.ias_matnet_load(weights.encode(), C.byref(net)), "ias_matnet_load")
+    try:
+        nf, nc = C.c_int32(0), C.c_int32(0)
+        check(lib.ias_matnet_shape(net, C.byref(nf), C.byref(nc)), "ias_matnet_shape")
+        a = np.ascontiguousarray(img_a, np.int64).ravel()
+        b = np.ascontiguousarray(img_b, np.int64).ravel()
+        f = np.ascontiguousarray(feats, np.float64)
+        assert f.size == nf.value, (f.size, nf.value)
+        probs = (C.c_float * nc.value)()
+        ch = C.c_int32(0)
+        check(lib.ias_matnet_predict(net, _ptr(a, C.c_int64), _ptr(b, C.c_int64), _ptr(f, C.c_double), probs,
+                                     C.byref(ch)), "ias_matnet_predict")
+        return int(ch.value), np.array(probs[:], np.float64)
+    finally:
+        lib.ias_matnet_free(net)

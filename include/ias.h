@@ -32,8 +32,9 @@
 extern "C" {
 #endif
 
-#define IAS_ABI_VERSION 3   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
-                               3: ias_csr_mul_csr_into (single pass) */
+#define IAS_ABI_VERSION 4   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
+                               3: ias_csr_mul_csr_into (single pass);
+                               4: input-aware selector (features, images, MatNet) */
 
 typedef enum ias_status {
     IAS_SUCCESS = 0,
@@ -253,6 +254,36 @@ ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_c
  * complete.  order: ias_order. */
 ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, const ias_csr *B, ias_csr *C,
                                 int32_t order, ias_report *report);
+
+/* ---------------------------------------------------------------- input-aware selector
+ * The "IA" of IA-SpGEMM (main.cpp:512-704; GPU/main.cu:272-460): matrix
+ * features and two 128x128 density images (A's and B's) go to MatNet, a small
+ * Keras CNN (MatNet.py Pred), whose argmax names the algorithm to run.  Host
+ * code (device matrices are copied to the host), off the timed path. */
+#define IAS_IMAGE_SIDE 128
+typedef struct ias_matnet ias_matnet;
+/* nfeatures 26 (the CPU program, main.cpp:651-679): GetInfo1(A) [0..8],
+ * GetInfo1(B) [9..17] (csr:257-287), GetInfo2(DIA(A)) [18..20], GetInfo2(DIA(B))
+ * [21..23] (dia:222-233), GetInfo3(ELL(A)) [24], GetInfo3(ELL(B)) [25]
+ * (ell:222-229); nfeatures 18 (the GPU program, GPU/main.cu:434-444):
+ * GetInfo1(A), GetInfo1(B).  Integer products the reference forms in `int`
+ * (row*col) are formed in double (the reference overflows beyond 2^31). */
+ias_status ias_features(const ias_csr *A, const ias_csr *B, int32_t nfeatures, double *features);
+/* main.cpp:516-565: image[k*128 + m] = number of A's entries mapped to cell
+ * (k, m) (rows/cols scaled to 128; sides under 128 spread over several cells). */
+ias_status ias_density_image(const ias_csr *A, int64_t *image);
+/* weights: "intel" / "amd" (the CPU program's sets: 26 features, 5 classes =
+ * algorithms {MKL, CSR, DIA, ELL, COO}), "p100" (the GPU program's: 18
+ * features, 3 classes = {CUSP, cuSPARSE, NSPARSE}), or a path to a blob made
+ * by tools/matnet_export.py; named sets are read from $IAS_MATNET_DIR or
+ * <dir of libias.so>/data. */
+ias_status ias_matnet_load(const char *weights, ias_matnet **net);
+ias_status ias_matnet_free(ias_matnet *net);
+ias_status ias_matnet_shape(const ias_matnet *net, int32_t *nfeatures, int32_t *nclasses);
+/* MatNet.py Pred: images scaled to 255*count/max, float32 forward pass,
+ * softmax into probs (nclasses, may be NULL); *chosen = argmax, 0-based. */
+ias_status ias_matnet_predict(const ias_matnet *net, const int64_t *image_a, const int64_t *image_b,
+                              const double *features, float *probs, int32_t *chosen);
 
 /* ---------------------------------------------------------------- verification */
 /* GetFlop (csr/common_csr.h:290-304): sum over stored A(i,j) of nnz(B row j). */

@@ -385,3 +385,64 @@ void ora_free_csr(ora_csr *A) { free(A->row_ptr); free(A->col); free(A->val); me
 void ora_free_coo(ora_coo *A) { free(A->row_offset); free(A->row); free(A->col); free(A->val); memset(A, 0, sizeof *A); }
 void ora_free_ell(ora_ell *A) { free(A->nnz_row); free(A->col); free(A->val); memset(A, 0, sizeof *A); }
 void ora_free_dia(ora_dia *A) { free(A->diagonal_offsets); free(A->diagonal_ind); free(A->val); memset(A, 0, sizeof *A); }
+
+/* ------------------------------------------------------------------ selector inputs
+ * GetInfo1 (csr:257-287): param5/6 start from row 0's length (csr:263-264),
+ * param7 = nnz/row, param8 = sum (n - param7)^2 / (row - 1), param9 =
+ * sqrt(param8) / param7. */
+static void ora_info1(const ora_csr *A, double *f) {
+    int64_t m = A->rows;
+    double p7 = (A->nnz + 0.0) / (double)m;
+    int64_t p5 = m > 0 ? A->row_ptr[1] - A->row_ptr[0] : 0, p6 = p5;
+    double p8 = 0.0;
+    for (int64_t i = 0; i < m; ++i) {
+        int64_t n = A->row_ptr[i + 1] - A->row_ptr[i];
+        p5 = p5 > n ? p5 : n;
+        p6 = p6 < n ? p6 : n;
+        p8 += ((double)n - p7) * ((double)n - p7);
+    }
+    p8 = p8 / (double)(m - 1);
+    f[0] = (double)A->rows; f[1] = (double)A->cols; f[2] = (double)A->nnz;
+    f[3] = (A->nnz + 0.0) / ((double)A->rows * (double)A->cols);
+    f[4] = (double)p5; f[5] = (double)p6; f[6] = p7; f[7] = p8; f[8] = sqrt(p8) / p7;
+}
+
+void ora_features(const ora_csr *A, const ora_csr *B, int32_t nfeatures, double *f) {
+    const ora_csr *M[2] = {A, B};
+    for (int i = 0; i < nfeatures; ++i) f[i] = 0.0;
+    ora_info1(A, f);
+    ora_info1(B, f + 9);
+    if (nfeatures != 26) return;
+    for (int t = 0; t < 2; ++t) {
+        ora_dia d;
+        ora_csr_to_dia(M[t], &d, 1e-300);   /* counts the diagonals, builds nothing */
+        f[18 + 3 * t] = d.num_diagonals;
+        f[19 + 3 * t] = (d.num_diagonals + 0.0) / (double)(M[t]->rows + M[t]->cols - 1);
+        f[20 + 3 * t] = ((double)d.num_diagonals * (double)M[t]->rows) / ((double)M[t]->rows * (double)M[t]->cols);
+        ora_free_dia(&d);
+        ora_ell e;
+        ora_csr_to_ell(M[t], &e, 1e-300);
+        f[24 + t] = (M[t]->nnz + 0.0) / ((double)M[t]->rows * (double)e.max_nnz_per_row);
+        ora_free_ell(&e);
+    }
+}
+
+/* main.cpp:520-565: cells [i*128/row, + 128/row] x [j*128/col, + 128/col]
+ * when a side is under 128, one cell when over, the identity at 128. */
+void ora_density_image(const ora_csr *A, int64_t *img) {
+    memset(img, 0, sizeof(int64_t) * 128 * 128);
+    for (int64_t i = 0; i < A->rows; ++i)
+        for (int64_t jj = A->row_ptr[i]; jj < A->row_ptr[i + 1]; ++jj) {
+            int64_t old_i = i, old_j = A->col[jj];
+            int64_t is = 0, ie = 0, js = 0, je = 0;
+            if (A->rows > 128) { is = old_i * 128 / A->rows; ie = is; }
+            else if (A->rows < 128) { is = old_i * 128 / A->rows; ie = is + 128 / A->rows; }
+            else { is = old_i; ie = old_i; }
+            if (A->cols > 128) { js = old_j * 128 / A->cols; je = js; }
+            else if (A->cols < 128) { js = old_j * 128 / A->cols; je = js + 128 / A->cols; }
+            else { js = old_j; je = old_j; }
+            for (int64_t k = is; k <= ie; ++k)
+                for (int64_t m = js; m <= je; ++m)
+                    if (k < 128 && m < 128) img[k * 128 + m]++;
+        }
+}

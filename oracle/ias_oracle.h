@@ -17,6 +17,15 @@
  *   ora_csr_to_dia     detail/dia/common_dia.h:29-96   (CSRtoDIA)
  *   ora_dia_mul_dia    detail/dia/common_dia.h:101-195 (DIA_mul_DIA)
  *   ora_sizeof_*       sizeofcsr/coo/ell/dia
+ *   ora_features       main.cpp:651-679 (GetInfo1/2/3: the selector's input)
+ *   ora_density_image  main.cpp:516-565 (MatNet's density images)
+ *
+ * Integer products the reference forms in `int` (row*col in GetInfo1/2,
+ * row*max_nnz_per_row in GetInfo3, old_i*128 in the image) overflow there for
+ * large inputs (undefined behaviour); here they are formed in int64/double,
+ * which agrees with the reference wherever it is defined.  The features are
+ * pinned by the reference's own printout for Inputs/dia.mtx (CPU/1.jpg,
+ * GPU/2.jpg: tests/golden/matnet_known_answers.json).
  *
  * Parity pinning: the reference kernels cannot be built in this image (every
  * detail/<fmt>/common_<fmt>.h includes "mkl.h", which the image lacks), so this restatement is
@@ -75,6 +84,14 @@ double  ora_sizeof_csr(const ora_csr *A);
 double  ora_sizeof_coo(const ora_coo *A);
 double  ora_sizeof_ell(const ora_ell *A);
 double  ora_sizeof_dia(const ora_dia *A);
+/* features[0..25] in main.cpp:651-679's layout (nfeatures 26) or GPU/main.cu:
+   434-444's (18): GetInfo1 of A and B (csr/common_csr.h:257-287), GetInfo2 of
+   DIA(A), DIA(B) (dia/common_dia.h:222-233; num_diagonals as CSRtoDIA counts
+   it, :32-49), GetInfo3 of ELL(A), ELL(B) (ell/common_ell.h:222-229;
+   max_nnz_per_row as CSRtoELL, :33-39). */
+void    ora_features(const ora_csr *A, const ora_csr *B, int32_t nfeatures, double *features);
+/* 128x128 density image, main.cpp:516-565 (row-major, image[k*128+m]) */
+void    ora_density_image(const ora_csr *A, int64_t *image);
 void    ora_free_csr(ora_csr *A);
 void    ora_free_coo(ora_coo *A);
 void    ora_free_ell(ora_ell *A);

@@ -65,6 +65,8 @@ for name, res, args in [
     ("ora_sizeof_coo", C.c_double, [P(OCoo)]),
     ("ora_sizeof_ell", C.c_double, [P(OEll)]),
     ("ora_sizeof_dia", C.c_double, [P(ODia)]),
+    ("ora_features", None, [P(OCsr), P(OCsr), C.c_int32, f64p]),
+    ("ora_density_image", None, [P(OCsr), i64p]),
     ("ora_free_csr", None, [P(OCsr)]),
     ("ora_free_coo", None, [P(OCoo)]),
     ("ora_free_ell", None, [P(OEll)]),
@@ -196,3 +198,17 @@ def gate_choices(A: Mat, gate=50.0):
          lib.ora_csr_to_dia(C.byref(a), C.byref(di), gate) == 0)
     lib.ora_free_coo(C.byref(co)); lib.ora_free_ell(C.byref(el)); lib.ora_free_dia(C.byref(di))
     return r
+
+
+def features(A: Mat, B: Mat, n: int = 26):
+    a, b = A.struct(), B.struct()
+    out = np.zeros(n, np.float64)
+    lib.ora_features(C.byref(a), C.byref(b), n, out.ctypes.data_as(f64p))
+    return out
+
+
+def density_image(A: Mat):
+    a = A.struct()
+    out = np.zeros(128 * 128, np.int64)
+    lib.ora_density_image(C.byref(a), out.ctypes.data_as(i64p))
+    return out.reshape(128, 128)
