@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
     p.add_argument("--engine", default="twophase", choices=["onepass", "twophase"])
+    p.add_argument("--as-rank", type=int, default=None,
+                   help="single process: run only rank R's shard of the --gpus N workload "
+                        "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers)")
     return p.parse_args()
 
 
@@ -108,10 +111,13 @@ def main():
     if rank == 0:
         A = generate(kind, prm)
         meta[:] = torch.tensor([A.rows, A.cols, A.nnz, ias.flops(A, A)])
-        bounds = (C.c_int64 * (world + 1))()
+        nparts = world_req if (args.as_rank is not None and not dist_on) else world
+        bounds = (C.c_int64 * (nparts + 1))()
         sa = A.struct()
-        ias.check(ias.lib.ias_partition_rows(C.byref(sa), C.byref(sa), world, bounds), "partition")
+        ias.check(ias.lib.ias_partition_rows(C.byref(sa), C.byref(sa), nparts, bounds), "partition")
         bnd = torch.tensor(list(bounds), dtype=torch.int64)
+        if nparts != world:   # --as-rank: this process is rank R of nparts
+            bnd = bnd[args.as_rank:args.as_rank + 2].clone()
     else:
         A = None
         bnd = torch.zeros(world + 1, dtype=torch.int64)
@@ -297,7 +303,15 @@ def main():
         "setup_s": round(t_gen, 2),
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind in ("rmat", "band", "ell"):
+    if args.as_rank is not None and not dist_on:
+        out["as_rank"] = {"rank": args.as_rank, "of": world_req, "rows": [r0, r1],
+                          "note": "one rank's shard only: value / nnz_per_s are per-rank figures"}
+        shard_flops = int(rep_s.flops) if args.engine == "twophase" else int(rep.flops)
+        out["as_rank"]["flops"] = shard_flops
+        out["value"] = round(2.0 * shard_flops / (ms_step * 1e6), 3)
+        out["n_gpus"] = 1
+    if rank == 0 and world == 1 and args.as_rank is None and not args.no_cpu_baseline and \
+            kind in ("rmat", "band", "ell"):
         out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
         if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
             out["speedup_vs_cpu_baseline"] = round(gflops / out["cpu_baseline"]["value"], 2)

@@ -345,13 +345,21 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
     IAS_TRY(HA.get(A));
     IAS_TRY(HB.get(B));
     const ias_csr *a = HA.m, *b = HB.m;
+    // Estimated device cost per row, in tenths of a product: a fixed cost per
+    // row (binning, launch share) plus its products, those of rows beyond
+    // the LDS bins (hash-partitioned, > 10922 products) weighted 2.1x.
+    // Calibrated on MI355X from K3' and two ranks of the 8-GPU scale-23 run
+    // (15.6 ps per product, 33 ps per partitioned-row product, 0.57 ns per row;
+    // DESIGN.md §6), so the rank holding R-MAT's hub rows gets fewer of them.
+    constexpr int64_t ROW_COST = 370, SMALL = 10, BIG = 21, PART_MIN = 10922;
     std::vector<int64_t> pref((size_t)a->rows + 1, 0);
     for (int64_t i = 0; i < a->rows; ++i) {
-        int64_t w = 1;   // +1 per row so empty rows still spread
+        int64_t prod = 0;
         for (int64_t p = a->row_ptr[i]; p < a->row_ptr[i + 1]; ++p) {
             const int32_t j = a->col[p];
-            w += b->row_ptr[j + 1] - b->row_ptr[j];
+            prod += b->row_ptr[j + 1] - b->row_ptr[j];
         }
+        const int64_t w = ROW_COST + prod * (prod > PART_MIN ? BIG : SMALL);
         pref[(size_t)i + 1] = pref[(size_t)i] + w;
     }
     const int64_t total = pref[(size_t)a->rows];

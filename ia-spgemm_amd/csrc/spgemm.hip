@@ -77,14 +77,17 @@ __device__ __forceinline__ unsigned long long block_excl_u64(unsigned long long 
 
 // Per-row allocation sizes of a binned row: bitmap words, duplicate slots,
 // partition items, global-table slots.
-__device__ __forceinline__ void bin_needs(const BinSpec &sp, int b, int32_t k, unsigned long long (&q)[4]) {
-    q[0] = q[1] = q[2] = q[3] = 0ull;
+constexpr int NQ = 5;   // per-row allocations: bitmap words, duplicate slots, partition items,
+                        // global-table slots, partition-bucket pairs
+__device__ __forceinline__ void bin_needs(const BinSpec &sp, int b, int32_t k, unsigned long long (&q)[NQ]) {
+    q[0] = q[1] = q[2] = q[3] = q[4] = 0ull;
     if (b <= 0) return;
     if (sp.ft) q[0] = (unsigned long long)((k + 31) / 32);
     const int32_t dc = dcap_of(sp, b, k);
     if (dc > 0) q[1] = (unsigned long long)dc;
     if (b == sp.nval + 1) {
         q[2] = (unsigned long long)nparts_of(k, sp.part_cap);
+        if (sp.ft) q[4] = (unsigned long long)k;   // symbolic: the row's products, bucketed by partition
     } else if (b == sp.nval + 2) {
         const unsigned long long need = (unsigned long long)k + ((unsigned long long)k + 1) / 2;
         unsigned long long S = 1;
@@ -101,32 +104,33 @@ template <int BLOCK, int R>
 __device__ __forceinline__ void count_bins(const BinSpec &sp, const int (&b)[R], const int32_t (&k)[R],
                                            Counters *cnt) {
     __shared__ int hist[MAX_BINS];
-    __shared__ unsigned long long red[4][BLOCK / WAVE];
+    __shared__ unsigned long long red[NQ][BLOCK / WAVE];
     for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK) hist[i] = 0;
     __syncthreads();
-    unsigned long long q[4] = {0ull, 0ull, 0ull, 0ull};   // bm_words, dup_slots, items, ws_slots
+    unsigned long long q[NQ] = {0ull, 0ull, 0ull, 0ull, 0ull};   // bin_needs order
 #pragma unroll
     for (int i = 0; i < R; ++i) {
         if (b[i] > 0) {
             atomicAdd(&hist[b[i]], 1);
-            unsigned long long n[4];
+            unsigned long long n[NQ];
             bin_needs(sp, b[i], k[i], n);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) q[j] += n[j];
+            for (int j = 0; j < NQ; ++j) q[j] += n[j];
         }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NQ; ++j)
 #pragma unroll
         for (int d = WAVE / 2; d > 0; d >>= 1) q[j] += __shfl_xor(q[j], d);
     if ((threadIdx.x & (WAVE - 1)) == 0)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[j][threadIdx.x / WAVE] = q[j];
+        for (int j = 0; j < NQ; ++j) red[j][threadIdx.x / WAVE] = q[j];
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < NQ) {
         unsigned long long t = 0;
         for (int i = 0; i < BLOCK / WAVE; ++i) t += red[threadIdx.x][i];
-        unsigned long long *dst[4] = {&cnt->bm_words, &cnt->dup_slots, &cnt->items, &cnt->ws_slots};
+        unsigned long long *dst[NQ] = {&cnt->bm_words, &cnt->dup_slots, &cnt->items, &cnt->ws_slots,
+                                       &cnt->part_prod};
         if (t) atomicAdd(dst[threadIdx.x], t);
     }
     for (int i = threadIdx.x; i < MAX_BINS; i += BLOCK)
@@ -297,12 +301,13 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
                                                            PartItem *items, int64_t *bm_off,
                                                            int64_t *ws_off, int64_t *dup_off,
                                                            int32_t *dupn, int32_t *nnz_row,
-                                                           const int64_t *qstart, Counters *cnt) {
+                                                           const int64_t *qstart, Counters *cnt,
+                                                           int64_t *pfirst, int64_t *pboff) {
     __shared__ int hist[MAX_BINS];
     __shared__ int64_t base[MAX_BINS];
     __shared__ int64_t bin_start[MAX_BINS];
     __shared__ unsigned long long red[BIN_BLOCK / WAVE];
-    __shared__ unsigned long long cbase[4];
+    __shared__ unsigned long long cbase[NQ];
     const int t = threadIdx.x;
     if (t < MAX_BINS) hist[t] = 0;
     if (t == 0) {
@@ -316,7 +321,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     const int part_bin = spec.nval + 1, wide_bin = spec.nval + 2;
     int b[BIN_RPT], local[BIN_RPT];
     int32_t k[BIN_RPT];
-    unsigned long long mine[4] = {0ull, 0ull, 0ull, 0ull};
+    unsigned long long mine[NQ] = {0ull, 0ull, 0ull, 0ull, 0ull};
 #pragma unroll
     for (int i = 0; i < BIN_RPT; ++i) {
         const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
@@ -329,29 +334,29 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
             if (b[i] == 0 && spec.zero_nnz) nnz_row[r] = 0;
             if (b[i] == 0 && dupn) dupn[r] = 0;
             if (b[i] > 0) local[i] = atomicAdd(&hist[b[i]], 1);
-            unsigned long long n[4];
+            unsigned long long n[NQ];
             bin_needs(spec, b[i], k[i], n);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mine[j] += n[j];
+            for (int j = 0; j < NQ; ++j) mine[j] += n[j];
         }
     }
     __syncthreads();
     if (t > 0 && t < MAX_BINS && hist[t] > 0) base[t] = atomicAdd(&cnt->cursor[t], hist[t]);
-    unsigned long long at[4], tot[4];
+    unsigned long long at[NQ], tot[NQ];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) at[j] = block_excl_u64<BIN_BLOCK>(mine[j], tot[j], red);
-    if (t < 4) {
-        unsigned long long *cur[4] = {&cnt->bm_cur, &cnt->dup_cur, &cnt->items_cur, &cnt->ws_cur};
+    for (int j = 0; j < NQ; ++j) at[j] = block_excl_u64<BIN_BLOCK>(mine[j], tot[j], red);
+    if (t < NQ) {
+        unsigned long long *cur[NQ] = {&cnt->bm_cur, &cnt->dup_cur, &cnt->items_cur, &cnt->ws_cur, &cnt->pb_cur};
         cbase[t] = tot[t] ? atomicAdd(cur[t], tot[t]) : 0ull;
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) at[j] += cbase[j];
+    for (int j = 0; j < NQ; ++j) at[j] += cbase[j];
 #pragma unroll
     for (int i = 0; i < BIN_RPT; ++i) {
         if (b[i] <= 0) continue;
         const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
-        unsigned long long n[4];
+        unsigned long long n[NQ];
         bin_needs(spec, b[i], k[i], n);
         const int64_t within = base[b[i]] + local[i];
         RowRef ref;
@@ -372,6 +377,8 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         if (b[i] == part_bin) {
             const uint32_t np = (uint32_t)n[2];
             for (uint32_t q = 0; q < np; ++q) items[at[2] + q] = PartItem{ref, q, np};
+            if (pfirst) pfirst[r] = (int64_t)at[2];
+            if (pboff) pboff[r] = (int64_t)at[4];
             if (spec.zero_nnz) nnz_row[r] = 0;
             // partitioned rows: a duplicate counter (k_dup_place decides the path)
             if (dupn) dupn[r] = spec.part_dcap_div > 0 ? 0 : -1;
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
             ws_off[within] = (int64_t)at[3];
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) at[j] += n[j];
+        for (int j = 0; j < NQ; ++j) at[j] += n[j];
     }
 }
 
@@ -495,11 +502,110 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
 
 // One workgroup per (row, hash partition): distinct columns of the partition
 // (added to nnz_row) and the first-touch bits of the row's bitmap.
+// Partition buckets: one workgroup per partitioned row reads its expansion
+// once and scatters (column, product) pairs into per-partition buckets
+// (count, scan, scatter in LDS), so that each partition's workgroup reads only
+// its own products instead of rescanning the whole row.  Rows with more than
+// PB_MAXP partitions keep the rescan (span len -1).
+constexpr int PB_BLOCK = 1024;
+constexpr int PB_MAXP = 4096;
+__global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(const int32_t *tcol, const RowRef *list, int32_t count,
+                                                          const int64_t *pfirst, const int64_t *pboff,
+                                                          int32_t part_cap, uint2 *bucket, PartSpan *spans) {
+    __shared__ uint32_t cnt[PB_MAXP];
+    __shared__ int scratch[32];
+    const RowRef ref = list[blockIdx.x];
+    const uint32_t np = nparts_of(ref.n, part_cap);
+    const int64_t it0 = pfirst[ref.row];
+    const int tid = threadIdx.x;
+    if (np > (uint32_t)PB_MAXP) {
+        for (uint32_t q = tid; q < np; q += PB_BLOCK) spans[it0 + q] = PartSpan{0, -1, 0};
+        return;
+    }
+    for (uint32_t q = tid; q < np; q += PB_BLOCK) cnt[q] = 0u;
+    __syncthreads();
+    const int32_t *pc = tcol + ref.q0;
+    // wave-aggregated LDS atomics: one per (wave, partition present), not per
+    // product (a row has few partitions, so per-product atomics all collide)
+    const bool direct = np >= 32;   // many partitions: plain LDS atomics rarely collide
+    auto wave_add = [&](bool active, uint32_t q) -> uint32_t {
+        if (direct) return active ? atomicAdd(&cnt[q], 1u) : 0u;
+        uint32_t rank = 0;
+        uint64_t todo = __ballot(active);
+        while (todo) {
+            const uint32_t q0 = (uint32_t)__shfl((int)q, __builtin_ctzll(todo));
+            const uint64_t same = __ballot(active && q == q0);
+            const int leader = __builtin_ctzll(same);
+            uint32_t base = 0;
+            if (__lane_id() == (uint32_t)leader) base = atomicAdd(&cnt[q0], (uint32_t)__popcll(same));
+            base = (uint32_t)__shfl((int)base, leader);
+            if (active && q == q0) rank = base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
+            todo &= ~same;
+        }
+        return rank;
+    };
+    constexpr int U = 4;   // products per thread in flight
+    for (int32_t p0 = 0; p0 < ref.n; p0 += U * PB_BLOCK) {
+        int32_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t p = p0 + u * PB_BLOCK + tid;
+            c[u] = p < ref.n ? ld_stream(pc + p) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool act = p0 + u * PB_BLOCK + tid < ref.n;
+            wave_add(act, act ? part_of(c[u], np) : 0u);
+        }
+    }
+    __syncthreads();
+    // exclusive scan of the counts (np <= PB_MAXP: PB_MAXP / PB_BLOCK per thread)
+    constexpr int PER = PB_MAXP / PB_BLOCK;
+    uint32_t v[PER], s = 0;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t q = (uint32_t)(tid * PER + i);
+        v[i] = q < np ? cnt[q] : 0u;
+        s += v[i];
+    }
+    int tot;
+    const int ex = Team<PB_BLOCK>::excl_sum((int)s, tot, scratch);
+    __syncthreads();
+    const int64_t base = pboff[ref.row];
+    uint32_t run = (uint32_t)ex;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t q = (uint32_t)(tid * PER + i);
+        if (q < np) {
+            spans[it0 + q] = PartSpan{base + run, (int32_t)v[i], 0};
+            cnt[q] = run;   // cursor
+        }
+        run += v[i];
+    }
+    __syncthreads();
+    for (int32_t p0 = 0; p0 < ref.n; p0 += U * PB_BLOCK) {
+        int32_t c[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t p = p0 + u * PB_BLOCK + tid;
+            c[u] = p < ref.n ? ld_stream(pc + p) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t p = p0 + u * PB_BLOCK + tid;
+            const bool act = p < ref.n;
+            const uint32_t at = wave_add(act, act ? part_of(c[u], np) : 0u);
+            if (act) bucket[base + at] = make_uint2((uint32_t)c[u], (uint32_t)p);
+        }
+    }
+}
+
 template <int TEAM, int K, int LOG2S>
 __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, const PartItem *items,
                                                         Bitmap bm, int32_t *nnz_row, uint2 *gpairs,
                                                         const int64_t *dup_off, int32_t *dupn,
-                                                        int32_t div, int32_t dmax, int *overflow) {
+                                                        int32_t div, int32_t dmax, int *overflow,
+                                                        const uint2 *bucket, const PartSpan *spans) {
     __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
     __shared__ uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
@@ -510,9 +616,14 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
     SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
     const uint32_t cap = div > 0 ? (uint32_t)min(it.ref.n / div, dmax) : 0u;
-    const int32_t n = symbolic_part_row<TEAM, K>(tcol, it.ref, tb, it.part, it.nparts, scratch, lbits,
-                                                 gbits, cap > 0 ? gpairs + dup_off[row] : nullptr,
-                                                 dupn + row, cap, overflow);
+    const PartSpan sp = spans ? spans[blockIdx.x] : PartSpan{0, -1, 0};
+    const int32_t n =
+        sp.len >= 0 ? symbolic_bucket_row<TEAM, K>(bucket + sp.start, sp.len, tb, scratch, lbits, gbits,
+                                                   cap > 0 ? gpairs + dup_off[row] : nullptr, dupn + row, cap,
+                                                   overflow)
+                    : symbolic_part_row<TEAM, K>(tcol, it.ref, tb, it.part, it.nparts, scratch, lbits, gbits,
+                                                 cap > 0 ? gpairs + dup_off[row] : nullptr, dupn + row, cap,
+                                                 overflow);
     // publish this partition's first-touch words (one atomic per non-zero word)
     const int64_t W = min<int64_t>(LBITS_WORDS, ((int64_t)it.ref.n + 31) / 32);
     for (int64_t w = threadIdx.x; w < W; w += TEAM)
@@ -1087,7 +1198,10 @@ static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per
 constexpr int32_t SYM_MAX = 10922;
 constexpr int32_t VAL_MAX = 5460;
 constexpr int32_t DW_MAX = 10922;
-constexpr int32_t SYM_PART_CAP = 10922;   // products per symbolic partition (16384-slot table)
+#ifndef SYM_PART_LOG2S
+#define SYM_PART_LOG2S 14   // table slots of a symbolic partition (2^14 = 128 KB of LDS)
+#endif
+constexpr int32_t SYM_PART_CAP = ((1 << SYM_PART_LOG2S) * 2) / 3;   // products per symbolic partition
 constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
 static_assert(DW_MAX >= SYM_MAX, "numeric partitions need the symbolic bitmap");
@@ -1217,6 +1331,13 @@ static int64_t resident_blocks(F kernel, int threads, size_t lds) {
     std::lock_guard<std::mutex> g(mu);
     cache[key] = v;
     return v;
+}
+
+// IAS_PART_BUCKET=0: partitioned rows rescan their expansion per partition
+// instead of bucketing it once (k_part_bucket).
+static bool part_bucket() {
+    const char *e = getenv("IAS_PART_BUCKET");
+    return !(e && *e == '0');
 }
 
 // IAS_SYM_PERSIST=1: symbolic teams persist over their bin (grid = resident
@@ -1542,6 +1663,10 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
 
     // ---- symbolic binning + symbolic
     IAS_TRY(reserve(B_SITEM, sizeof(PartItem) * (size_t)(c1.items + 1)));
+    IAS_TRY(reserve(B_PFIRST, sizeof(int64_t) * (size_t)(rows + 1)));
+    IAS_TRY(reserve(B_PBOFF, sizeof(int64_t) * (size_t)(rows + 1)));
+    IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
+    if (part_bucket()) IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -1557,7 +1682,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if (rows > 0)
         k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
-            as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc);
+            as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc, as<int64_t>(bufs[B_PFIRST]),
+            as<int64_t>(bufs[B_PBOFF]));
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
     HIPC(hipEventRecord(ev[1], s));
     int64_t st[MAX_BINS];
@@ -1567,9 +1693,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int lane_no = 0;
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        k_symbolic_part<1024, 8, 14><<<(unsigned)c1.items, 1024, 0, t>>>(
+        const bool pb = part_bucket();
+        if (pb)
+            k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
+                                                 as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
+                                                 as<PartSpan>(bufs[B_PSPAN]));
+        k_symbolic_part<1024, 8, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow);
+            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, pb ? as<uint2>(bufs[B_PBKT]) : nullptr,
+            pb ? as<PartSpan>(bufs[B_PSPAN]) : nullptr);
         k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
         k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
                                       sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
@@ -1600,7 +1732,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
-            nullptr, dc2);
+            nullptr, dc2, nullptr, nullptr);
     CHECK_LAUNCH("numeric binning", s);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
@@ -1950,7 +2082,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
     k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
                                                                   lists, nullptr, nullptr, offs, nullptr,
-                                                                  nullptr, nullptr, nullptr, dc);
+                                                                  nullptr, nullptr, nullptr, dc, nullptr, nullptr);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));

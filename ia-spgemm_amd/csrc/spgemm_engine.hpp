@@ -38,6 +38,7 @@ struct Counters {
     unsigned long long dup_slots; // duplicate-list slots
     unsigned long long st_prod, st_nnz;   // products / C entries of the streaming rows
     unsigned long long items_cur, bm_cur, ws_cur, dup_cur;   // scatter-pass cursors
+    unsigned long long part_prod, pb_cur;   // products of partitioned rows (bucket space) + cursor
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
@@ -55,7 +56,9 @@ struct ias_plan {
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4,
         // single-pass path (onepass)
         B_OPCF, B_OPBF, B_OPCID, B_OPBPOS, B_OPCROW, B_OPSTAT, B_OPMISC, B_OPBROW, B_OPBLEN, B_OPBPTR,
-        B_OPBCOL, B_OPBVAL, B_OPBCPTR, B_COUNT
+        B_OPBCOL, B_OPBVAL, B_OPBCPTR,
+        // partition buckets of the symbolic pass
+        B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN, B_COUNT
     };
     struct Buf {
         void *p = nullptr;

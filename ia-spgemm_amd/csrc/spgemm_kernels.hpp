@@ -140,6 +140,14 @@ struct PartItem {
     uint32_t part;
     uint32_t nparts;
 };
+// The products of one partition, bucketed: pairs (column, product index) at
+// bucket[start .. start + len); len < 0: not bucketed (the partition rescans
+// the row's expansion).
+struct PartSpan {
+    int64_t start;
+    int32_t len;
+    int32_t pad;
+};
 
 // Where row i of C goes: CSR/COO (start = ptr[i]) or ELL (start = i*stride);
 // len[i] = nnz of row i (from the symbolic pass).
@@ -635,6 +643,88 @@ __device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const 
         }
     }
     TM::sync();
+    for (uint32_t s = lane; s < S; s += TEAM)
+        if (table.key[s] != EMPTY_KEY) {
+            const uint32_t p = table.minp[s];
+            if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+            else atomicOr(&gbits[p >> 5], 1u << (p & 31));
+        }
+    TM::sync();
+    if (full) atomicOr(overflow, 1);
+    return TM::sum(created, scratch);
+}
+
+// Slot of a column known to be in a table filled by insert_k's bucketed
+// probing (the column sits in its home bucket or in one of the full buckets
+// after it).
+__device__ __forceinline__ int table_find(const int32_t *key, uint32_t S, int32_t c) {
+    const uint32_t nb = S >> 2;
+    uint32_t b = slot_hash(c, nb);
+    for (uint32_t probe = 0; probe < nb; ++probe) {
+        const int4 q = ((const int4 *)key)[b];
+        if (q.x == c) return (int)(4 * b);
+        if (q.y == c) return (int)(4 * b + 1);
+        if (q.z == c) return (int)(4 * b + 2);
+        if (q.w == c) return (int)(4 * b + 3);
+        b = (b + 1u == nb) ? 0u : b + 1u;
+    }
+    return -1;
+}
+
+// symbolic_part_row over a bucketed partition: the pairs (column, product)
+// of this partition only, in no particular order — so first touches are final
+// only after every insert, and the duplicates are listed in a second pass.
+template <int TEAM, int K>
+__device__ __forceinline__ int32_t symbolic_bucket_row(const uint2 *bk, int32_t bn, const SymTable<true> &table,
+                                                       int *scratch, uint32_t *lbits, uint32_t *gbits,
+                                                       uint2 *pairs, int32_t *dcnt, uint32_t cap, int *overflow) {
+    using TM = Team<TEAM>;
+    const int lane = TM::lane();
+    const uint32_t S = table.size;
+    for (uint32_t s = lane; s < S; s += TEAM) {
+        table.key[s] = EMPTY_KEY;
+        table.minp[s] = 0xFFFFFFFFu;
+    }
+    TM::sync();
+    int created = 0;
+    bool full = false;
+    for (int i0 = 0; i0 < bn; i0 += TEAM * K) {
+        int32_t c[K];
+        uint32_t pp[K];
+        bool use[K];
+        int slot[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = i0 + k * TEAM + lane;
+            use[k] = i < bn;
+            const uint2 e = use[k] ? bk[i] : make_uint2((uint32_t)EMPTY_KEY, 0u);
+            c[k] = (int32_t)e.x;
+            pp[k] = e.y;
+        }
+        insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
+    }
+    TM::sync();
+    if (pairs && !full) {
+        for (int i0 = 0; i0 < bn; i0 += TEAM) {
+            const int i = i0 + lane;
+            bool dup = false;
+            uint32_t p = 0, m = 0;
+            if (i < bn) {
+                const uint2 e = bk[i];
+                p = e.y;
+                const int s = table_find(table.key, S, (int32_t)e.x);
+                m = table.minp[s];
+                dup = m != p;
+            }
+            const uint64_t b = __ballot(dup);
+            if (b == 0ull) continue;
+            int base = 0;
+            if ((__lane_id()) == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(dcnt, __popcll(b));
+            base = __shfl(base, __builtin_ctzll(b));
+            const uint32_t j = (uint32_t)base + (uint32_t)__popcll(b & ((1ull << __lane_id()) - 1ull));
+            if (dup && j < cap) pairs[j] = make_uint2(p, m);
+        }
+    }
     for (uint32_t s = lane; s < S; s += TEAM)
         if (table.key[s] != EMPTY_KEY) {
             const uint32_t p = table.minp[s];

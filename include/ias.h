@@ -299,8 +299,11 @@ ias_status ias_sum_dia(const ias_dia *A, double *sum);
  * Row-block view [r0, r1) of A without copying (row_ptr is an offset view;
  * kernels address col/val absolutely, so no rebasing is needed). */
 ias_status ias_csr_row_view(const ias_csr *A, int64_t r0, int64_t r1, ias_csr *view);
-/* Split A's rows into nparts contiguous blocks with near-equal products
- * (flops prefix); bounds has nparts+1 entries. Host or device A. */
+/* Split A's rows into nparts contiguous blocks of near-equal estimated device
+ * cost (a flops prefix, not rows; each row weighted by a fixed
+ * per-row cost plus its products, products of hash-partitioned rows counted
+ * 2.1x, calibrated on MI355X); bounds has nparts+1 entries.
+ * Host or device A. */
 ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int32_t nparts,
                               int64_t *bounds);
 /* Add `offset` to every entry of a device row pointer (allgatherv fix-up). */
