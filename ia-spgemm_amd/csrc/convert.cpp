@@ -1,7 +1,8 @@
 // convert.cpp — format layer (CSRtoCOO/ELL/DIA and back), transpose, size
 // models, verified sums, GetFlop and flops-balanced row partitioning.
-// Host code; device operands are staged through the host (these are not on
-// the timed path: the reference times conversions separately as trans_time).
+// CSR -> COO/ELL/DIA of a device-resident CSR run on the device
+// (convert_dev.hip); everything else here is host code that stages device
+// operands through the host (not on the timed path).
 #include "ias.h"
 #include "ias_internal.hpp"
 
@@ -68,6 +69,7 @@ extern "C" double ias_sizeof_dia(const ias_dia *A) {
 // ------------------------------------------------------------------ CSR -> X
 extern "C" ias_status ias_csr_to_coo(const ias_csr *A, ias_coo *out, double gate) {
     if (!A || !out) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->memory == IAS_MEMORY_DEVICE) return csr_to_coo_device(A, out, gate);
     HostCsr H;
     IAS_TRY(H.get(A));
     const ias_csr *M = H.m;
@@ -104,6 +106,7 @@ extern "C" ias_status ias_csr_to_coo(const ias_csr *A, ias_coo *out, double gate
 
 extern "C" ias_status ias_csr_to_ell(const ias_csr *A, ias_ell *out, double gate) {
     if (!A || !out) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->memory == IAS_MEMORY_DEVICE) return csr_to_ell_device(A, out, gate);
     HostCsr H;
     IAS_TRY(H.get(A));
     const ias_csr *M = H.m;
@@ -143,6 +146,7 @@ extern "C" ias_status ias_csr_to_ell(const ias_csr *A, ias_ell *out, double gate
 // stored entry lies on it; a later duplicate (i,j) overwrites an earlier one.
 extern "C" ias_status ias_csr_to_dia(const ias_csr *A, ias_dia *out, double gate) {
     if (!A || !out) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->memory == IAS_MEMORY_DEVICE) return csr_to_dia_device(A, out, gate);
     HostCsr H;
     IAS_TRY(H.get(A));
     const ias_csr *M = H.m;

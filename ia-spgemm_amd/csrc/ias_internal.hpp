@@ -39,6 +39,12 @@ ias_status ias_sort_rows_ell_device(ias_plan *plan, const int32_t *nnz_row, int6
                                     int32_t K, int32_t *col, double *val);
 ias_status ias_shift_device(int64_t *p, int64_t n, int64_t off, void *stream);
 
+// CSR -> COO / ELL / DIA for a device-resident CSR (convert_dev.hip); outputs
+// on the same device, byte-identical to the host conversions in convert.cpp.
+ias_status csr_to_coo_device(const ias_csr *A, ias_coo *out, double gate);
+ias_status csr_to_ell_device(const ias_csr *A, ias_ell *out, double gate);
+ias_status csr_to_dia_device(const ias_csr *A, ias_dia *out, double gate);
+
 }  // namespace ias
 
 #define IAS_TRY(expr)                                   \

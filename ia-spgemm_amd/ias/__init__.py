@@ -271,6 +271,11 @@ def mtx_read(path: str):
     return csr_to_numpy(m), info
 
 
+def mtx_write(path: str, A: HostCsr) -> None:
+    sa = A.struct()
+    check(lib.ias_mtx_write(path.encode(), C.byref(sa)), f"ias_mtx_write({path})")
+
+
 def mtx_read_pair(path_a: str, path_b: str):
     a, b, ia, ib = Csr(), Csr(), MtxInfo(), MtxInfo()
     check(lib.ias_mtx_read_pair(path_a.encode(), path_b.encode(), C.byref(a), C.byref(b),

@@ -350,6 +350,89 @@ def test_dia(case, inputs_dir):
     ias.lib.ias_dia_free(C.byref(dc))
 
 
+# ------------------------------------------------------------------ device-side conversions (f3)
+def _dup_matrix():
+    """Rows with repeated columns (later duplicate wins in CSRtoDIA) and empty rows."""
+    rp = np.array([0, 3, 3, 6, 6, 8], np.int64)
+    col = np.array([1, 1, 4, 0, 2, 0, 3, 3], np.int32)
+    val = np.array([1.5, -2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0])
+    return ias.HostCsr(5, 6, rp, col, val)
+
+
+CONV_CASES = [("dia.mtx", None), ("small.mtx", None),
+              ("band", lambda: ias.gen_band(3000, 4, seed=5)),
+              ("rmat12", lambda: ias.gen_rmat(12, 8, seed=3)),
+              ("dups", _dup_matrix),
+              ("empty", lambda: ias.HostCsr(7, 9, np.zeros(8, np.int64), np.zeros(0, np.int32), np.zeros(0)))]
+
+_CONV = {"coo": (ias.Coo, "ias_csr_to_coo", "ias_coo_copy", "ias_coo_free"),
+         "ell": (ias.Ell, "ias_csr_to_ell", "ias_ell_copy", "ias_ell_free"),
+         "dia": (ias.Dia, "ias_csr_to_dia", "ias_dia_copy", "ias_dia_free")}
+
+
+def _conv_arrays(kind, m):
+    """All arrays of a host-resident converted matrix, as numpy."""
+    if kind == "coo":
+        n = m.nnz
+        return dict(rp=ias._np(m.row_offset, m.rows + 1, np.int64), r=ias._np(m.row, n, np.int32),
+                    c=ias._np(m.col, n, np.int32), v=bits(ias._np(m.val, n, np.float64)))
+    if kind == "ell":
+        rk = m.rows * m.max_nnz_per_row
+        return dict(K=m.max_nnz_per_row, n=ias._np(m.nnz_row, m.rows, np.int32),
+                    c=ias._np(m.col, rk, np.int32), v=bits(ias._np(m.val, rk, np.float64)))
+    nd = m.num_diagonals
+    return dict(nd=nd, off=ias._np(m.diagonal_offsets, nd, np.int32),
+                ind=ias._np(m.diagonal_ind, max(m.rows + m.cols - 1, 0), np.int32),
+                v=bits(ias._np(m.val, m.rows * nd, np.float64)))
+
+
+def _convert(kind, src, gate=0.0):
+    T, conv, copy, free = _CONV[kind]
+    out = T()
+    st = getattr(ias.lib, conv)(C.byref(src), C.byref(out), gate)
+    if st != 0:
+        return st, None, (out.rows, out.cols, out.choice)
+    if out.memory == ias.MEMORY_DEVICE:
+        h = T()
+        ias.check(getattr(ias.lib, copy)(C.byref(out), C.byref(h), ias.MEMORY_HOST, 0), "copy back")
+        getattr(ias.lib, free)(C.byref(out))
+        out = h
+    arrays = _conv_arrays(kind, out)
+    meta = (out.rows, out.cols, out.choice)
+    getattr(ias.lib, free)(C.byref(out))
+    return st, arrays, meta
+
+
+@pytest.mark.parametrize("kind", ["coo", "ell", "dia"])
+@pytest.mark.parametrize("case", CONV_CASES, ids=lambda c: c[0])
+def test_device_conversions(case, kind, inputs_dir):
+    """CSRtoCOO/ELL/DIA of a device CSR (convert_dev.hip) == the host conversion, byte for byte,
+    for the whole matrix and for a row view (row_ptr[0] != 0)."""
+    name, mk = case
+    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
+    hs = A.struct()
+    dA = ias.Csr()
+    ias.check(ias.lib.ias_csr_copy(C.byref(hs), C.byref(dA), ias.MEMORY_DEVICE, 0), "copy")
+    try:
+        lo, hi = (A.rows // 3, A.rows - A.rows // 4) if A.rows > 2 else (0, A.rows)
+        hv, dv = ias.Csr(), ias.Csr()
+        ias.check(ias.lib.ias_csr_row_view(C.byref(hs), lo, hi, C.byref(hv)), "view")
+        ias.check(ias.lib.ias_csr_row_view(C.byref(dA), lo, hi, C.byref(dv)), "view")
+        for host_src, dev_src in ((hs, dA), (hv, dv)):
+            sh, want, mh = _convert(kind, host_src)
+            sd, got, md = _convert(kind, dev_src)
+            assert sh == sd == 0 and mh == md, (name, kind, sh, sd, mh, md)
+            for k in want:
+                np.testing.assert_array_equal(np.asarray(got[k]), np.asarray(want[k]), err_msg=f"{name} {kind} {k}")
+        # the size gate (coo/ell/dia common headers): same verdict both sides
+        for gate in (0.5, 1.0, 4.0):
+            sh, _, mh = _convert(kind, hs, gate)
+            sd, _, md = _convert(kind, dA, gate)
+            assert sh == sd and mh[2] == md[2], (name, kind, gate, sh, sd)
+    finally:
+        ias.lib.ias_csr_free(C.byref(dA))
+
+
 # ------------------------------------------------------------------ device-resident two-phase
 def test_two_phase_device_resident():
     A = ias.gen_rmat(14, 16, seed=4)

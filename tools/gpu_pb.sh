@@ -8,7 +8,7 @@ OUT=gpurun_out/${TAG:-pb}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
-for pb in 1 0 1; do export IAS_SYM_PACK=$pb;
+for pb in 1 0 1; do export IAS_PART_BUCKET=$pb;
   timeout -k 10 300 python bench.py --no-cpu-baseline --steps 5 --warmup 2 > $OUT/bench_pb$pb.json 2>> $OUT/bench.err || exit 1
   python3 -c "import json; d=json.load(open('$OUT/bench_pb$pb.json')); print('pb$pb', d['value'], d['ms_per_step'], d['phases_ms_rank0'])"
 done
