@@ -6,9 +6,10 @@
 //   1 IAS row-wise hash, reference order (byte-identical to CSR_MUL_CSR)
 //   2 IAS row-wise hash + per-row sort (sorted columns, as csrgemm emits)
 // Usage: spgemm-gpu A.mtx [--aat] [--rand10] [--seed N] [--mtx-out C.mtx]
-//   default C = A*A (the README's contract); --aat builds B = A^T as
-//   main.cu:260-269 (mkl_dcsrcsc); --rand10 replaces values by rand()%10 as
-//   main.cu:236-243, seeded by --seed (the reference seeds with time(NULL)).
+//   default C = A*A (the README's contract); --aat builds B = A^T on the
+//   device, as main.cu:260-269 does with mkl_dcsrcsc; --rand10 replaces
+//   values by rand()%10 as main.cu:236-243, seeded by --seed (the reference
+//   seeds with time(NULL)).
 #include "ias.h"
 #include "report.hpp"
 
@@ -38,8 +39,17 @@ int main(int argc, char **argv) {
         srand(seed);
         for (int64_t i = 0; i < A.nnz; ++i) A.val[i] = rand() % 10;
     }
-    if (aat) CLI_TRY("transpose", ias_csr_transpose(&A, &B));
-    else CLI_TRY("copy", ias_csr_copy(&A, &B, IAS_MEMORY_HOST, 0));
+    // A goes to HBM once; A^T is built there (device transpose replacing
+    // mkl_dcsrcsc) and brought back only for the selector's features.
+    ias_csr dA{}, dB{};
+    CLI_TRY("upload", ias_csr_copy(&A, &dA, IAS_MEMORY_DEVICE, 0));
+    if (aat) {
+        CLI_TRY("transpose", ias_csr_transpose(&dA, &dB));
+        CLI_TRY("copy", ias_csr_copy(&dB, &B, IAS_MEMORY_HOST, 0));
+    } else {
+        CLI_TRY("copy", ias_csr_copy(&A, &B, IAS_MEMORY_HOST, 0));
+        CLI_TRY("upload", ias_csr_copy(&B, &dB, IAS_MEMORY_DEVICE, 0));
+    }
     int64_t flops = 0;
     CLI_TRY("flops", ias_flops(&A, &B, &flops));
 
@@ -49,9 +59,6 @@ int main(int argc, char **argv) {
     const int chosen = cli::matnet_choose(A, B, 18, "p100", 1);
     std::printf("The Chosen One = Algorithm %d\n", chosen + 1);
 
-    ias_csr dA{}, dB{};
-    CLI_TRY("upload", ias_csr_copy(&A, &dA, IAS_MEMORY_DEVICE, 0));
-    CLI_TRY("upload", ias_csr_copy(&B, &dB, IAS_MEMORY_DEVICE, 0));
     ias_opts o;
     ias_opts_default(&o);
     o.output_memory = IAS_MEMORY_DEVICE;

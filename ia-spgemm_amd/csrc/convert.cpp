@@ -1,7 +1,7 @@
 // convert.cpp — format layer (CSRtoCOO/ELL/DIA and back), transpose, size
 // models, verified sums, GetFlop and flops-balanced row partitioning.
-// CSR -> COO/ELL/DIA of a device-resident CSR run on the device
-// (convert_dev.hip); everything else here is host code that stages device
+// CSR -> COO/ELL/DIA and the transpose of a device-resident CSR run on the
+// device (convert_dev.hip); everything else here is host code that stages device
 // operands through the host (not on the timed path).
 #include "ias.h"
 #include "ias_internal.hpp"
@@ -271,6 +271,7 @@ extern "C" ias_status ias_dia_to_csr(const ias_dia *A, ias_csr *out) {
 // Aᵀ by a stable counting sort on column (rows of Aᵀ ascend by source row).
 extern "C" ias_status ias_csr_transpose(const ias_csr *A, ias_csr *AT) {
     if (!A || !AT) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->memory == IAS_MEMORY_DEVICE) return csr_transpose_device(A, AT);
     HostCsr H;
     IAS_TRY(H.get(A));
     const ias_csr *M = H.m;

@@ -118,6 +118,30 @@ __global__ __launch_bounds__(CV_BLOCK) void k_cv_dia_vals(const int64_t *__restr
         for (int64_t p = rp[r]; p < rp[r + 1]; ++p) dval[r * nd + slot[(rows - r) + col[p]]] = val[p];
 }
 
+__global__ __launch_bounds__(CV_BLOCK) void k_cv_col_count(const int32_t *__restrict__ col, int64_t nnz,
+                                                           unsigned long long *__restrict__ cnt) {
+    for (int64_t p = (int64_t)blockIdx.x * CV_BLOCK + threadIdx.x; p < nnz; p += (int64_t)gridDim.x * CV_BLOCK)
+        atomicAdd(&cnt[col[p]], 1ull);
+}
+
+__global__ __launch_bounds__(CV_BLOCK) void k_cv_iota(int32_t *__restrict__ idx, int64_t n) {
+    for (int64_t p = (int64_t)blockIdx.x * CV_BLOCK + threadIdx.x; p < n; p += (int64_t)gridDim.x * CV_BLOCK)
+        idx[p] = (int32_t)p;
+}
+
+// Aᵀ entry k = A entry idx[k] (idx sorted stably by column): column = its row.
+__global__ __launch_bounds__(CV_BLOCK) void k_cv_t_gather(const int32_t *__restrict__ idx,
+                                                          const int32_t *__restrict__ row,
+                                                          const double *__restrict__ val, int64_t nnz,
+                                                          int32_t *__restrict__ tcol,
+                                                          double *__restrict__ tval) {
+    for (int64_t k = (int64_t)blockIdx.x * CV_BLOCK + threadIdx.x; k < nnz; k += (int64_t)gridDim.x * CV_BLOCK) {
+        const int32_t e = idx[k];
+        tcol[k] = row[e];
+        tval[k] = val[e];
+    }
+}
+
 double csr_bytes_dev(const ias_csr *A) {
     return 4.0 * (double)(A->rows + 1 + A->nnz + 3) + 8.0 * (double)A->nnz;
 }
@@ -268,6 +292,67 @@ ias_status csr_to_dia_device(const ias_csr *A, ias_dia *out, double gate) {
         return IAS_ERROR_DEVICE;
     }
     *out = D;
+    return IAS_SUCCESS;
+}
+
+// Aᵀ (mkl_dcsrcsc in GPU/main.cu:260-269; host counting sort in convert.cpp):
+// column counts -> row pointers, and a stable LSD radix sort of the entry
+// indices by column, so each row of Aᵀ lists source rows in ascending order
+// (duplicates in stored order), exactly as the host counting sort.
+ias_status csr_transpose_device(const ias_csr *A, ias_csr *AT) {
+    DHIPC(hipSetDevice(A->device));
+    if (A->nnz > (int64_t)INT32_MAX) return IAS_ERROR_OVERFLOW;
+    int64_t base = 0;
+    IAS_TRY(dev_copy_d2h(&base, A->row_ptr, sizeof(int64_t), A->device));
+    const int64_t nnz = A->nnz, cols = A->cols;
+    ias_csr T{};
+    IAS_TRY(ias_csr_alloc(&T, A->cols, A->rows, nnz, IAS_MEMORY_DEVICE, A->device));
+    DevBuf cnt, row, kin, kout, iin, iout, tmp;
+    cnt.device = row.device = kin.device = kout.device = iin.device = iout.device = tmp.device = A->device;
+    ias_status s = IAS_SUCCESS;
+    auto fail = [&](ias_status st) {
+        ias_csr_free(&T);
+        return st;
+    };
+    if ((s = dev_alloc(&cnt.p, sizeof(unsigned long long) * (size_t)(cols + 1), A->device)) != IAS_SUCCESS ||
+        (s = dev_memset(cnt.p, 0, sizeof(unsigned long long) * (size_t)(cols + 1), A->device)) != IAS_SUCCESS ||
+        (s = dev_alloc(&row.p, sizeof(int32_t) * (size_t)nnz, A->device)) != IAS_SUCCESS ||
+        (s = dev_alloc(&iin.p, sizeof(int32_t) * (size_t)nnz, A->device)) != IAS_SUCCESS ||
+        (s = dev_alloc(&iout.p, sizeof(int32_t) * (size_t)nnz, A->device)) != IAS_SUCCESS ||
+        (s = dev_alloc(&kout.p, sizeof(int32_t) * (size_t)nnz, A->device)) != IAS_SUCCESS)
+        return fail(s);
+    const int32_t *col = A->col + base;
+    const double *val = A->val + base;
+    if (nnz > 0) {
+        hipLaunchKernelGGL(k_cv_col_count, dim3(grid_for(nnz, CV_BLOCK)), dim3(CV_BLOCK), 0, 0, col, nnz,
+                           (unsigned long long *)cnt.p);
+        hipLaunchKernelGGL(k_cv_coo_rows, dim3(grid_for(A->rows, CV_BLOCK / CV_GROUP)), dim3(CV_BLOCK), 0, 0,
+                           A->row_ptr, A->rows, (int32_t *)row.p);
+        hipLaunchKernelGGL(k_cv_iota, dim3(grid_for(nnz, CV_BLOCK)), dim3(CV_BLOCK), 0, 0, (int32_t *)iin.p, nnz);
+    }
+    // row_ptr of Aᵀ = exclusive scan of the column counts (cols + 1 entries)
+    size_t tb = 0, tb2 = 0;
+    unsigned long long *cp = (unsigned long long *)cnt.p;
+    DHIPC(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cp, (unsigned long long *)T.row_ptr, (int)(cols + 1), 0));
+    int end_bit = 1;
+    while (end_bit < 31 && ((int64_t)1 << end_bit) < cols) ++end_bit;
+    DHIPC(hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, col, (int32_t *)kout.p, (const int32_t *)iin.p,
+                                             (int32_t *)iout.p, (int)nnz, 0, end_bit, 0));
+    if ((s = dev_alloc(&tmp.p, std::max(tb, tb2), A->device)) != IAS_SUCCESS) return fail(s);
+    tb = tb2 = std::max(tb, tb2);
+    DHIPC(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, cp, (unsigned long long *)T.row_ptr, (int)(cols + 1), 0));
+    if (nnz > 0) {
+        DHIPC(hipcub::DeviceRadixSort::SortPairs(tmp.p, tb2, col, (int32_t *)kout.p, (const int32_t *)iin.p,
+                                                 (int32_t *)iout.p, (int)nnz, 0, end_bit, 0));
+        hipLaunchKernelGGL(k_cv_t_gather, dim3(grid_for(nnz, CV_BLOCK)), dim3(CV_BLOCK), 0, 0,
+                           (const int32_t *)iout.p, (const int32_t *)row.p, val, nnz, T.col, T.val);
+    }
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess || hipGetLastError() != hipSuccess) {
+        set_last_error("csr_transpose_device: %s", hipGetErrorString(e));
+        return fail(IAS_ERROR_DEVICE);
+    }
+    *AT = T;
     return IAS_SUCCESS;
 }
 

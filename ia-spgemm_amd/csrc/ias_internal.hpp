@@ -44,6 +44,7 @@ ias_status ias_shift_device(int64_t *p, int64_t n, int64_t off, void *stream);
 ias_status csr_to_coo_device(const ias_csr *A, ias_coo *out, double gate);
 ias_status csr_to_ell_device(const ias_csr *A, ias_ell *out, double gate);
 ias_status csr_to_dia_device(const ias_csr *A, ias_dia *out, double gate);
+ias_status csr_transpose_device(const ias_csr *A, ias_csr *AT);
 
 }  // namespace ias
 

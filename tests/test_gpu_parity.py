@@ -433,6 +433,35 @@ def test_device_conversions(case, kind, inputs_dir):
         ias.lib.ias_csr_free(C.byref(dA))
 
 
+@pytest.mark.parametrize("case", CONV_CASES + [("rect", lambda: ias.HostCsr(
+    3, 70000, np.array([0, 2, 2, 5], np.int64), np.array([69999, 5, 5, 0, 69999], np.int32),
+    np.array([1.0, 2.0, 3.0, 4.0, 5.0])))], ids=lambda c: c[0])
+def test_device_transpose(case, inputs_dir):
+    """Aᵀ of a device CSR (stable radix sort, convert_dev.hip) == the host counting sort, byte for byte."""
+    name, mk = case
+    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
+    hs = A.struct()
+    dA = ias.Csr()
+    ias.check(ias.lib.ias_csr_copy(C.byref(hs), C.byref(dA), ias.MEMORY_DEVICE, 0), "copy")
+    try:
+        lo, hi = (A.rows // 3, A.rows) if A.rows > 2 else (0, A.rows)
+        hv, dv = ias.Csr(), ias.Csr()
+        ias.check(ias.lib.ias_csr_row_view(C.byref(hs), lo, hi, C.byref(hv)), "view")
+        ias.check(ias.lib.ias_csr_row_view(C.byref(dA), lo, hi, C.byref(dv)), "view")
+        for host_src, dev_src in ((hs, dA), (hv, dv)):
+            th, td = ias.Csr(), ias.Csr()
+            ias.check(ias.lib.ias_csr_transpose(C.byref(host_src), C.byref(th)), "host T")
+            ias.check(ias.lib.ias_csr_transpose(C.byref(dev_src), C.byref(td)), "device T")
+            assert td.memory == ias.MEMORY_DEVICE
+            want, got = ias.csr_to_numpy(th), ias.csr_to_numpy(td)
+            assert (got.rows, got.cols) == (want.rows, want.cols)
+            np.testing.assert_array_equal(got.row_ptr, want.row_ptr, err_msg=name)
+            np.testing.assert_array_equal(got.col, want.col, err_msg=name)
+            np.testing.assert_array_equal(bits(got.val), bits(want.val), err_msg=name)
+    finally:
+        ias.lib.ias_csr_free(C.byref(dA))
+
+
 # ------------------------------------------------------------------ device-resident two-phase
 def test_two_phase_device_resident():
     A = ias.gen_rmat(14, 16, seed=4)
