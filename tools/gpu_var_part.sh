@@ -14,7 +14,7 @@ for v in "${VS[@]}"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -ffp-contract=off -Wno-unused-value \
      -Iinclude -Iia-spgemm_amd/csrc $flags -c ia-spgemm_amd/csrc/spgemm.hip -o build_tim/spgemm_$name.o || exit 1
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_tim/libias_$name.so build_tim/spgemm_$name.o \
-     $O/ias_api.o $O/dia.o $O/mtx_io.o $O/gen.o $O/convert.o $O/mkl_baseline.o $O/matnet.o \
+     $O/ias_api.o $O/dia.o $O/convert_dev.o $O/mtx_io.o $O/gen.o $O/convert.o $O/mkl_baseline.o $O/matnet.o \
      -L/usr/lib/gcc/x86_64-linux-gnu/11 -lgomp -ldl || exit 1
 done
 for v in "${VS[@]}"; do
