@@ -607,11 +607,13 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
                                                         int32_t div, int32_t dmax, int *overflow,
                                                         const uint2 *bucket, const PartSpan *spans) {
     __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
-    __shared__ uint32_t minp[1 << LOG2S];
+    __shared__ __attribute__((aligned(16))) uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
     const PartItem it = items[blockIdx.x];
     const int64_t row = it.ref.row;
+    Timer tmr;
+    tmr.start();
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
     SymTable<true> tb{keys, minp, 1u << LOG2S};
     uint32_t *gbits = bm.bits + bm.off[row];
@@ -620,7 +622,7 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
     const int32_t n =
         sp.len >= 0 ? symbolic_bucket_row<TEAM, K>(bucket + sp.start, sp.len, tb, scratch, lbits, gbits,
                                                    cap > 0 ? gpairs + dup_off[row] : nullptr, dupn + row, cap,
-                                                   overflow)
+                                                   overflow, tmr)
                     : symbolic_part_row<TEAM, K>(tcol, it.ref, tb, it.part, it.nparts, scratch, lbits, gbits,
                                                  cap > 0 ? gpairs + dup_off[row] : nullptr, dupn + row, cap,
                                                  overflow);
@@ -629,6 +631,8 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
     for (int64_t w = threadIdx.x; w < W; w += TEAM)
         if (lbits[w]) atomicOr(&gbits[w], lbits[w]);
     if (threadIdx.x == 0 && n > 0) atomicAdd(&nnz_row[row], n);
+    tmr.mark(6);
+    tmr.flush(29, threadIdx.x == 0);   // slot 29: symbolic partitions
 }
 
 // Exclusive popcount prefix of each partitioned row's first-touch bitmap.
@@ -1698,7 +1702,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
                                                  as<PartSpan>(bufs[B_PSPAN]));
-        k_symbolic_part<1024, 8, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
+        k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
             PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, pb ? as<uint2>(bufs[B_PBKT]) : nullptr,
             pb ? as<PartSpan>(bufs[B_PSPAN]) : nullptr);

@@ -677,61 +677,130 @@ __device__ __forceinline__ int table_find(const int32_t *key, uint32_t S, int32_
 template <int TEAM, int K>
 __device__ __forceinline__ int32_t symbolic_bucket_row(const uint2 *bk, int32_t bn, const SymTable<true> &table,
                                                        int *scratch, uint32_t *lbits, uint32_t *gbits,
-                                                       uint2 *pairs, int32_t *dcnt, uint32_t cap, int *overflow) {
+                                                       uint2 *pairs, int32_t *dcnt, uint32_t cap, int *overflow,
+                                                       Timer &tm) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
     const uint32_t S = table.size;
-    for (uint32_t s = lane; s < S; s += TEAM) {
-        table.key[s] = EMPTY_KEY;
-        table.minp[s] = 0xFFFFFFFFu;
+    {
+        const uint4 ek = make_uint4((uint32_t)EMPTY_KEY, (uint32_t)EMPTY_KEY, (uint32_t)EMPTY_KEY,
+                                    (uint32_t)EMPTY_KEY);
+        const uint4 em = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        for (uint32_t s = lane; s < S / 4; s += TEAM) {
+            ((uint4 *)table.key)[s] = ek;
+            ((uint4 *)table.minp)[s] = em;
+        }
     }
+    if (lane == 0) scratch[60] = 0;   // duplicate counter of the one-step path
     TM::sync();
+    tm.mark(1);
     int created = 0;
     bool full = false;
-    for (int i0 = 0; i0 < bn; i0 += TEAM * K) {
+    auto first_touch = [&](uint32_t p) {
+        if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+        else atomicOr(&gbits[p >> 5], 1u << (p & 31));
+    };
+    // list the duplicates of one wave's items (dup: minp of the column != p)
+    auto list_dups = [&](bool dup, uint32_t p, uint32_t m) {
+        const uint64_t b = __ballot(dup);
+        if (b == 0ull) return;
+        int base = 0;
+        if ((__lane_id()) == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(dcnt, __popcll(b));
+        base = __shfl(base, __builtin_ctzll(b));
+        const uint32_t j = (uint32_t)base + (uint32_t)__popcll(b & ((1ull << __lane_id()) - 1ull));
+        if (dup && j < cap) pairs[j] = make_uint2(p, m);
+    };
+    if (bn <= TEAM * K) {
+        // one step: the items stay in registers with their slots, so the
+        // first-touch bits and the duplicates come from minp[slot] directly
+        // (no second read of the bucket, no table search, no slot scan)
         int32_t c[K];
         uint32_t pp[K];
         bool use[K];
         int slot[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int i = i0 + k * TEAM + lane;
+            const int i = k * TEAM + lane;
             use[k] = i < bn;
             const uint2 e = use[k] ? bk[i] : make_uint2((uint32_t)EMPTY_KEY, 0u);
             c[k] = (int32_t)e.x;
             pp[k] = e.y;
         }
         insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
-    }
-    TM::sync();
-    if (pairs && !full) {
-        for (int i0 = 0; i0 < bn; i0 += TEAM) {
-            const int i = i0 + lane;
-            bool dup = false;
-            uint32_t p = 0, m = 0;
-            if (i < bn) {
-                const uint2 e = bk[i];
-                p = e.y;
-                const int s = table_find(table.key, S, (int32_t)e.x);
-                m = table.minp[s];
-                dup = m != p;
-            }
+        tm.mark(2);
+        TM::sync();
+        tm.mark(3);
+        uint32_t m[K];   // all K reads in flight before the atomics
+#pragma unroll
+        for (int k = 0; k < K; ++k) m[k] = slot[k] >= 0 ? table.minp[slot[k]] : 0u;
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (slot[k] >= 0 && m[k] == pp[k]) first_touch(pp[k]);
+        // duplicates: ranks from an LDS counter, then one global atomic per
+        // workgroup for the row-wide base (a returning global atomic per wave
+        // and item serialised this pass)
+        int jl[K];
+        const bool listing = pairs && !full;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const bool dup = listing && slot[k] >= 0 && m[k] != pp[k];
             const uint64_t b = __ballot(dup);
+            jl[k] = -1;
             if (b == 0ull) continue;
             int base = 0;
-            if ((__lane_id()) == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(dcnt, __popcll(b));
+            if ((__lane_id()) == (uint32_t)__builtin_ctzll(b)) base = atomicAdd(&scratch[60], __popcll(b));
             base = __shfl(base, __builtin_ctzll(b));
-            const uint32_t j = (uint32_t)base + (uint32_t)__popcll(b & ((1ull << __lane_id()) - 1ull));
-            if (dup && j < cap) pairs[j] = make_uint2(p, m);
+            if (dup) jl[k] = base + __popcll(b & ((1ull << __lane_id()) - 1ull));
         }
+        tm.mark(4);
+        TM::sync();
+        if (lane == 0) scratch[61] = scratch[60] > 0 ? atomicAdd(dcnt, scratch[60]) : 0;
+        TM::sync();
+        const int gb = scratch[61];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (jl[k] >= 0 && (uint32_t)(gb + jl[k]) < cap) pairs[gb + jl[k]] = make_uint2(pp[k], m[k]);
+        tm.mark(5);
+    } else {
+        for (int i0 = 0; i0 < bn; i0 += TEAM * K) {
+            int32_t c[K];
+            uint32_t pp[K];
+            bool use[K];
+            int slot[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = i0 + k * TEAM + lane;
+                use[k] = i < bn;
+                const uint2 e = use[k] ? bk[i] : make_uint2((uint32_t)EMPTY_KEY, 0u);
+                c[k] = (int32_t)e.x;
+                pp[k] = e.y;
+            }
+            insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
+        }
+        tm.mark(2);
+        TM::sync();
+        tm.mark(3);
+        if (pairs && !full) {
+            for (int i0 = 0; i0 < bn; i0 += TEAM) {
+                const int i = i0 + lane;
+                bool dup = false;
+                uint32_t p = 0, m = 0;
+                if (i < bn) {
+                    const uint2 e = bk[i];
+                    p = e.y;
+                    const int s = table_find(table.key, S, (int32_t)e.x);
+                    m = table.minp[s];
+                    dup = m != p;
+                }
+                list_dups(dup, p, m);
+            }
+        }
+        tm.mark(4);
+        for (uint32_t s = lane; s < S; s += TEAM)
+            if (table.key[s] != EMPTY_KEY) first_touch(table.minp[s]);
+        TM::sync();
+        tm.mark(5);
     }
-    for (uint32_t s = lane; s < S; s += TEAM)
-        if (table.key[s] != EMPTY_KEY) {
-            const uint32_t p = table.minp[s];
-            if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
-            else atomicOr(&gbits[p >> 5], 1u << (p & 31));
-        }
-    TM::sync();
     if (full) atomicOr(overflow, 1);
     return TM::sum(created, scratch);
 }

@@ -49,6 +49,8 @@ def main():
         team = 1 << (slot % 16)
         if slot >= 30:
             kind, team = ("onepass" if slot == 31 else "op-big"), 512
+        elif slot == 29:
+            kind, team = "sym-part", 1024
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
         print("%-8s TEAM %4d rows %8d  per-row us: %s  sum %.2f" % (
             kind, team, cnt, " ".join("%6.2f" % u for u in us), sum(us)))
