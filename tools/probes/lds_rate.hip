@@ -25,6 +25,13 @@ __global__ __launch_bounds__(256) void k(unsigned *out, unsigned seed) {
         else if constexpr (OP == 5) { acc += tab[a]; tab[(a * 7) & (N - 1)] = acc; }   // read then write
         else if constexpr (OP == 6) acc += atomicCAS(&tab[a & ~3u], 0xFFFFFFFFu, x);   // 16 banks only
         else if constexpr (OP == 7) atomicMin(&tab[a & ~3u], x);
+        else if constexpr (OP == 8) { const uint4 q = ((const uint4 *)tab)[a >> 2]; acc += q.x ^ q.y ^ q.z ^ q.w; }
+        else if constexpr (OP == 9) { const uint2 q = ((const uint2 *)tab)[a >> 1]; acc += q.x ^ q.y; }
+        else if constexpr (OP == 10) {   // bucket insert chain: b128 read, CAS, min
+            const uint4 q = ((const uint4 *)tab)[a >> 2];
+            const unsigned v = atomicCAS(&tab[a & ~3u], q.x == 0xFFFFFFFFu ? 0xFFFFFFFFu : q.x, x);
+            atomicMin(&tab[(a & ~3u) ^ 1u], v);
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) out[blockIdx.x] = acc + tab[x & (N - 1)];
@@ -61,5 +68,8 @@ int main() {
     run<5>("read+write", d);
     run<6>("cas_rtn slot0-of-4", d);
     run<7>("min slot0-of-4", d);
+    run<8>("read_b128", d);
+    run<9>("read_b64", d);
+    run<10>("b128+cas+min chain", d);
     return 0;
 }
