@@ -195,7 +195,9 @@ ias_status ias_mtx_write(const char *path, const ias_csr *A);
  * dia/common_dia.h:56, ell/common_ell.h:47; 20 on GPU: GPU/detail/dia/
  * common_dia.h:51 etc.); <= 0 disables the gate.  When the gate fails the
  * output has choice = 0, no arrays, and IAS_ERROR_INFEASIBLE is returned.
- * Inputs may be host or device; outputs land in the same memory. */
+ * Inputs may be host or device; outputs land in the same memory.  A device
+ * CSR is converted on its device (no host round trip), byte-identical to the
+ * host conversion. */
 ias_status ias_csr_to_coo(const ias_csr *A, ias_coo *out, double gate); /* CSRtoCOO coo:29-66 */
 ias_status ias_csr_to_ell(const ias_csr *A, ias_ell *out, double gate); /* CSRtoELL ell:30-77 */
 ias_status ias_csr_to_dia(const ias_csr *A, ias_dia *out, double gate); /* CSRtoDIA dia:29-96 */
@@ -204,7 +206,8 @@ ias_status ias_ell_to_csr(const ias_ell *A, ias_csr *out);
 /* Every stored DIA position that is in range (explicit zeros included). */
 ias_status ias_dia_to_csr(const ias_dia *A, ias_csr *out);
 /* B = A^T, as mkl_dcsrcsc(job={0,0,0,0,0,1}) in GPU/main.cu:260-269; columns of
- * each output row ascend (stable by source row). */
+ * each output row ascend (stable by source row).  A device CSR is transposed
+ * on its device (stable radix sort), byte-identical to the host path. */
 ias_status ias_csr_transpose(const ias_csr *A, ias_csr *AT);
 
 /* size models of the report's memory_size column */
