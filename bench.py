@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
     p.add_argument("--engine", default="twophase", choices=["onepass", "twophase"])
+    p.add_argument("--no-host-e2e", action="store_true",
+                   help="skip the one PCIe-inclusive call with host operands (N=1 only)")
     p.add_argument("--as-rank", type=int, default=None,
                    help="single process: run only rank R's shard of the --gpus N workload "
                         "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers)")
@@ -315,6 +317,23 @@ def main():
         out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
         if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
             out["speedup_vs_cpu_baseline"] = round(gflops / out["cpu_baseline"]["value"], 2)
+
+    if rank == 0 and world == 1 and args.as_rank is None and not args.no_host_e2e:
+        # the end-to-end rate with host operands (A, B uploaded, C
+        # downloaded over PCIe inside the call), one call after the timed
+        # region; never `value`.
+        del c_ci, c_va
+        torch.cuda.empty_cache()
+        t_e = time.perf_counter()
+        _, rh = ias.spgemm(A, order=order, device=local)
+        wall = (time.perf_counter() - t_e) * 1e3
+        out["host_e2e"] = {
+            "what": "one ias_csr_mul_csr call with host A, B and host C (upload + compute + download); "
+                    "ms_wall also holds the call's workspace allocation and the numpy copy of C",
+            "ms_wall": round(wall, 2), "ms_upload": round(rh.ms_upload, 3),
+            "ms_device": round(rh.ms_total, 3), "ms_download": round(rh.ms_download, 3),
+            "gflops_pcie_inclusive": round(2.0 * flops_total / (wall * 1e6), 3),
+        }
 
     ias.lib.ias_plan_destroy(plan)
     if rank == 0:

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <memory>
 #include <vector>
@@ -416,6 +417,11 @@ bool onepass_fits(int64_t flops) {
     return 12.0 * (double)flops + 8.0 <= 0.5 * (double)fr;
 }
 
+// host wall clock (ms) for the synchronous PCIe staging of host operands
+double host_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 double ms_since(hipEvent_t a, hipEvent_t b) {
     float t = 0;
     hipEventElapsedTime(&t, a, b);
@@ -444,12 +450,14 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     // Operands not resident on the compute device are copied there (rebased,
     // so host row views work); resident ones, views included, are used as-is.
     StagedCsr sa, sb;
+    const double t_up = host_ms();
     IAS_TRY(sa.stage(A, plan->device));
     const ias_csr *dA = sa.get(), *dB = dA;
     if (B != A) {
         IAS_TRY(sb.stage(B, plan->device));
         dB = sb.get();
     }
+    if (rep && (sa.owned || sb.owned)) rep->ms_upload = host_ms() - t_up;
     dev::Rows ra{dA->row_ptr, nullptr, 0, dA->col, dA->val};
     dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
     ias_csr D{};
@@ -485,7 +493,9 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     HIPC(hipStreamSynchronize(s));
     if (out_mem == IAS_MEMORY_HOST) {
         ias_csr H{};
+        const double t_dn = host_ms();
         ias_status cs = ias_csr_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        if (rep) rep->ms_download = host_ms() - t_dn;
         ias_csr_free(&D);
         if (cs != IAS_SUCCESS) return cs;
         *C = H;
@@ -513,6 +523,7 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
     const int64_t *ap, *bp;
     const int32_t *ac, *bc;
     const double *av, *bv;
+    const double t_up = host_ms();
     IAS_TRY(st.stage(A->row_offset, A->rows + 1, A->memory, A->device, plan->device, &ap));
     IAS_TRY(st.stage(A->col, A->nnz, A->memory, A->device, plan->device, &ac));
     IAS_TRY(st.stage(A->val, A->nnz, A->memory, A->device, plan->device, &av));
@@ -523,6 +534,7 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
         IAS_TRY(st.stage(B->col, B->nnz, B->memory, B->device, plan->device, &bc));
         IAS_TRY(st.stage(B->val, B->nnz, B->memory, B->device, plan->device, &bv));
     }
+    if (rep && !st.owned.empty()) rep->ms_upload = host_ms() - t_up;
     dev::Rows ra{ap, nullptr, 0, ac, av};
     dev::Rows rb{bp, nullptr, 0, bc, bv};
     IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
@@ -555,7 +567,9 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
     HIPC(hipStreamSynchronize(s));
     if (out_mem == IAS_MEMORY_HOST) {
         ias_coo H{};
+        const double t_dn = host_ms();
         ias_status cs = ias_coo_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        if (rep) rep->ms_download = host_ms() - t_dn;
         ias_coo_free(&D);
         if (cs != IAS_SUCCESS) return cs;
         *C = H;
@@ -583,6 +597,7 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
     const int32_t *an, *bn, *ac, *bc;
     const double *av, *bv;
     const size_t ak = (size_t)A->rows * A->max_nnz_per_row, bk = (size_t)B->rows * B->max_nnz_per_row;
+    const double t_up = host_ms();
     IAS_TRY(st.stage(A->nnz_row, A->rows, A->memory, A->device, plan->device, &an));
     IAS_TRY(st.stage(A->col, ak, A->memory, A->device, plan->device, &ac));
     IAS_TRY(st.stage(A->val, ak, A->memory, A->device, plan->device, &av));
@@ -593,6 +608,7 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
         IAS_TRY(st.stage(B->col, bk, B->memory, B->device, plan->device, &bc));
         IAS_TRY(st.stage(B->val, bk, B->memory, B->device, plan->device, &bv));
     }
+    if (rep && !st.owned.empty()) rep->ms_upload = host_ms() - t_up;
     dev::Rows ra{nullptr, an, A->max_nnz_per_row, ac, av};
     dev::Rows rb{nullptr, bn, B->max_nnz_per_row, bc, bv};
     IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, (int64_t)ak, rep));
@@ -626,7 +642,9 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
     HIPC(hipStreamSynchronize(s));
     if (out_mem == IAS_MEMORY_HOST) {
         ias_ell H{};
+        const double t_dn = host_ms();
         ias_status cs = ias_ell_copy(&D, &H, IAS_MEMORY_HOST, 0);
+        if (rep) rep->ms_download = host_ms() - t_dn;
         ias_ell_free(&D);
         if (cs != IAS_SUCCESS) return cs;
         *C = H;

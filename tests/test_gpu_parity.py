@@ -615,3 +615,21 @@ def test_chunk_edges_all_paths():
     np.testing.assert_array_equal(bits(ias._np(cc.val, n, np.float64)), bits(refc.val))
     for m in (ca, cc):
         ias.lib.ias_coo_free(C.byref(m))
+
+
+def test_host_operand_transfer_times():
+    """Host operands: the report carries the PCIe staging times (ias.h ms_upload / ms_download)."""
+    A = ias.gen_rmat(12, 8, seed=5)
+    _, rep = ias.spgemm(A)
+    assert rep.ms_upload > 0 and rep.ms_download > 0 and rep.ms_total > 0
+    hs = A.struct()
+    dA = ias.Csr()
+    ias.check(ias.lib.ias_csr_copy(C.byref(hs), C.byref(dA), ias.MEMORY_DEVICE, 0), "copy")
+    try:
+        c, r2 = ias.Csr(), ias.Report()
+        o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=0)
+        ias.check(ias.lib.ias_csr_mul_csr(C.byref(dA), C.byref(dA), C.byref(c), C.byref(o), C.byref(r2)), "dev")
+        assert r2.ms_upload == 0 and r2.ms_download == 0
+        ias.lib.ias_csr_free(C.byref(c))
+    finally:
+        ias.lib.ias_csr_free(C.byref(dA))
