@@ -1384,6 +1384,17 @@ static void sym_launch(const Launch &l, const int32_t *tcol, uint32_t W, uint32_
                                                    a.dupn, a.dupt);
 }
 
+// items per lane of the multi-wave symbolic teams (a step of TEAM * K
+// products ends in a workgroup barrier)
+#ifndef SYM_K5
+#define SYM_K5 4
+#endif
+#ifndef SYM_K6
+#define SYM_K6 4
+#endif
+#ifndef SYM_K7
+#define SYM_K7 2
+#endif
 #ifndef SYM_WPE_SMALL
 #define SYM_WPE_SMALL 7   // waves per SIMD the register budget of the wave-level teams allows
 #endif
@@ -1395,9 +1406,9 @@ static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, u
         case 2: sym_launch<64, 4, 4, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
         case 3: sym_launch<64, 8, 4, 4>(l, tcol, W, D, nnz, a); break;
         case 4: sym_launch<128, 4, 1, 6>(l, tcol, W, D, nnz, a); break;
-        case 5: sym_launch<256, 4, 1, 1>(l, tcol, W, D, nnz, a); break;
-        case 6: sym_launch<512, 4, 1, 1>(l, tcol, W, D, nnz, a); break;
-        default: sym_launch<1024, 2, 1, 1>(l, tcol, W, D, nnz, a); break;
+        case 5: sym_launch<256, SYM_K5, 1, 1>(l, tcol, W, D, nnz, a); break;
+        case 6: sym_launch<512, SYM_K6, 1, 1>(l, tcol, W, D, nnz, a); break;
+        default: sym_launch<1024, SYM_K7, 1, 1>(l, tcol, W, D, nnz, a); break;
     }
 }
 
