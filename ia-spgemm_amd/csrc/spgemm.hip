@@ -393,7 +393,6 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
 // ---------------------------------------------------------------- symbolic kernels
 // LDS tables are sized per bin at launch (dynamic LDS, any slot count), so a
 // row costs only the bytes its bin needs and more rows are resident per CU.
-constexpr int LBITS_WORDS = 2048;   // first-touch bits staged in LDS (positions < 65536)
 
 __host__ __device__ constexpr size_t round16(size_t b) { return (b + 15) & ~size_t(15); }
 

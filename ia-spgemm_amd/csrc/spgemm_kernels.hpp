@@ -282,6 +282,12 @@ struct Team {
     }
 };
 
+// first-touch bits of a partitioned row staged in LDS by each partition's
+// workgroup (positions < 32 * LBITS_WORDS; later ones go to global atomics)
+#ifndef LBITS_WORDS
+#define LBITS_WORDS 2048
+#endif
+
 // table slot hash (multiply-shift onto [0, size), any size) and an
 // independent partition hash
 __device__ __forceinline__ uint32_t slot_hash(int32_t c, uint32_t size) {
@@ -646,7 +652,7 @@ __device__ __forceinline__ int32_t symbolic_part_row(const int32_t *tcol, const 
     for (uint32_t s = lane; s < S; s += TEAM)
         if (table.key[s] != EMPTY_KEY) {
             const uint32_t p = table.minp[s];
-            if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+            if ((p >> 5) < (uint32_t)LBITS_WORDS) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
             else atomicOr(&gbits[p >> 5], 1u << (p & 31));
         }
     TM::sync();
@@ -697,7 +703,7 @@ __device__ __forceinline__ int32_t symbolic_bucket_row(const uint2 *bk, int32_t 
     int created = 0;
     bool full = false;
     auto first_touch = [&](uint32_t p) {
-        if ((p >> 5) < 2048u) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
+        if ((p >> 5) < (uint32_t)LBITS_WORDS) atomicOr(&lbits[p >> 5], 1u << (p & 31));   // LDS staging
         else atomicOr(&gbits[p >> 5], 1u << (p & 31));
     };
     // list the duplicates of one wave's items (dup: minp of the column != p)
