@@ -246,6 +246,7 @@ ias_status csr_to_ell_device(const ias_csr *A, ias_ell *out, double gate) {
 ias_status csr_to_dia_device(const ias_csr *A, ias_dia *out, double gate) {
     DHIPC(hipSetDevice(A->device));
     const int64_t span = A->rows + A->cols;   // index (rows - i) + j in [1, span)
+    if (span + 1 > (int64_t)INT32_MAX) return IAS_ERROR_OVERFLOW;   // hipcub scan length is int
     DevBuf flag, slot, tmp;
     flag.device = slot.device = tmp.device = A->device;
     IAS_TRY(dev_alloc(&flag.p, sizeof(int32_t) * (size_t)(span + 1), A->device));
@@ -301,7 +302,7 @@ ias_status csr_to_dia_device(const ias_csr *A, ias_dia *out, double gate) {
 // (duplicates in stored order), exactly as the host counting sort.
 ias_status csr_transpose_device(const ias_csr *A, ias_csr *AT) {
     DHIPC(hipSetDevice(A->device));
-    if (A->nnz > (int64_t)INT32_MAX) return IAS_ERROR_OVERFLOW;
+    if (A->nnz > (int64_t)INT32_MAX || A->cols + 1 > (int64_t)INT32_MAX) return IAS_ERROR_OVERFLOW;
     int64_t base = 0;
     IAS_TRY(dev_copy_d2h(&base, A->row_ptr, sizeof(int64_t), A->device));
     const int64_t nnz = A->nnz, cols = A->cols;
