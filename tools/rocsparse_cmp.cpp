@@ -1,0 +1,168 @@
+// rocSPARSE csrgemm beside the engine, for context.
+// Same K3' matrix (R-MAT 2^20, edge factor 20, seed 2), C = A*A in fp64,
+// device-resident inputs, both sides timed as nnz stage + compute stage with
+// their workspace allocated once outside the timed loop; C arrays sized once
+// at flops(A*A).  rocSPARSE emits columns sorted inside each row, so the
+// engine runs with IAS_ORDER_SORTED here; columns must match exactly, values
+// within 1e-12 relative (rocSPARSE sums in its own order).
+//   build: see tools/rocsparse_cmp.sh
+#include <hip/hip_runtime.h>
+#include <rocsparse/rocsparse.h>
+#include "ias.h"
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
+#define RC(x) do { rocsparse_status s_ = (x); if (s_ != rocsparse_status_success) { \
+    fprintf(stderr, "%s:%d rocsparse status %d\n", __FILE__, __LINE__, (int)s_); exit(1); } } while (0)
+#define IC(x) do { ias_status s_ = (x); if (s_ != IAS_SUCCESS) { \
+    fprintf(stderr, "%s:%d ias %s: %s\n", __FILE__, __LINE__, ias_status_string(s_), ias_last_error()); exit(1); } } while (0)
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char **argv) {
+    int scale = argc > 1 ? atoi(argv[1]) : 20;
+    int steps = argc > 2 ? atoi(argv[2]) : 5;
+    ias_csr Ah{}, A{};
+    IC(ias_gen_rmat(scale, 20.0, 0.45, 0.15, 0.15, 2, 0, &Ah));
+    IC(ias_csr_copy(&Ah, &A, IAS_MEMORY_DEVICE, 0));
+    int64_t flops = 0;
+    IC(ias_flops(&Ah, &Ah, &flops));
+    const int64_t n = A.rows, nnz_a = A.nnz;
+    printf("rmat scale %d: rows %lld nnz(A) %lld flops %lld\n", scale, (long long)n,
+           (long long)nnz_a, (long long)flops);
+
+    // ---- engine: two-phase on a plan; reference order (the bench's order) then sorted
+    ias_plan *plan = nullptr;
+    IC(ias_plan_create(&plan, 0, nullptr));
+    ias_csr Ce{};
+    IC(ias_csr_alloc(&Ce, n, n, flops, IAS_MEMORY_DEVICE, 0));
+    const int64_t cap = Ce.nnz;
+    int64_t nnz_e = 0;
+    double best_e = 1e30, sum_e = 0, best_eref = 1e30;
+    for (int it = -2; it < steps; ++it) {
+        HC(hipDeviceSynchronize());
+        double t0 = now_ms();
+        IC(ias_csr_mul_csr_nnz(plan, &A, &A, &nnz_e, nullptr, nullptr));
+        Ce.nnz = cap;
+        IC(ias_csr_mul_csr_compute(plan, &A, &A, &Ce, IAS_ORDER_REFERENCE, nullptr));
+        HC(hipDeviceSynchronize());
+        double t = now_ms() - t0;
+        if (it >= 0 && t < best_eref) best_eref = t;
+    }
+    for (int it = -2; it < steps; ++it) {
+        HC(hipDeviceSynchronize());
+        double t0 = now_ms();
+        IC(ias_csr_mul_csr_nnz(plan, &A, &A, &nnz_e, nullptr, nullptr));
+        Ce.nnz = cap;
+        IC(ias_csr_mul_csr_compute(plan, &A, &A, &Ce, IAS_ORDER_SORTED, nullptr));
+        HC(hipDeviceSynchronize());
+        double t = now_ms() - t0;
+        if (it >= 0) { sum_e += t; if (t < best_e) best_e = t; }
+    }
+
+    // ---- rocSPARSE generic spgemm (i64 row pointers, i32 columns, f64)
+    rocsparse_handle h;
+    RC(rocsparse_create_handle(&h));
+    rocsparse_spmat_descr dA, dC, dD;
+    RC(rocsparse_create_csr_descr(&dA, n, n, nnz_a, A.row_ptr, A.col, A.val,
+                                  rocsparse_indextype_i64, rocsparse_indextype_i32,
+                                  rocsparse_index_base_zero, rocsparse_datatype_f64_r));
+    int64_t *rp_r = nullptr; int32_t *col_r = nullptr; double *val_r = nullptr;
+    HC(hipMalloc(&rp_r, (n + 1) * sizeof(int64_t)));
+    HC(hipMalloc(&col_r, flops * sizeof(int32_t)));
+    HC(hipMalloc(&val_r, flops * sizeof(double)));
+    RC(rocsparse_create_csr_descr(&dC, n, n, 0, rp_r, nullptr, nullptr,
+                                  rocsparse_indextype_i64, rocsparse_indextype_i32,
+                                  rocsparse_index_base_zero, rocsparse_datatype_f64_r));
+    int64_t *rp_d = nullptr;  // D = 0 (beta is NULL); its row pointer must still exist
+    HC(hipMalloc(&rp_d, (n + 1) * sizeof(int64_t)));
+    HC(hipMemset(rp_d, 0, (n + 1) * sizeof(int64_t)));
+    RC(rocsparse_create_csr_descr(&dD, n, n, 0, rp_d, nullptr, nullptr,
+                                  rocsparse_indextype_i64, rocsparse_indextype_i32,
+                                  rocsparse_index_base_zero, rocsparse_datatype_f64_r));
+    const double alpha = 1.0;
+    size_t bsz = 0;
+    RC(rocsparse_spgemm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, dA, dA,
+                        nullptr, dD, dC, rocsparse_datatype_f64_r, rocsparse_spgemm_alg_default,
+                        rocsparse_spgemm_stage_buffer_size, &bsz, nullptr));
+    void *buf = nullptr;
+    HC(hipMalloc(&buf, bsz > 0 ? bsz : 4));
+    int64_t nnz_r = 0;
+    double best_r = 1e30, sum_r = 0;
+    for (int it = -2; it < steps; ++it) {
+        HC(hipDeviceSynchronize());
+        double t0 = now_ms();
+        RC(rocsparse_spgemm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, dA, dA,
+                            nullptr, dD, dC, rocsparse_datatype_f64_r, rocsparse_spgemm_alg_default,
+                            rocsparse_spgemm_stage_nnz, &bsz, buf));
+        int64_t r, c;
+        RC(rocsparse_spmat_get_size(dC, &r, &c, &nnz_r));
+        RC(rocsparse_csr_set_pointers(dC, rp_r, col_r, val_r));
+        RC(rocsparse_spgemm(h, rocsparse_operation_none, rocsparse_operation_none, &alpha, dA, dA,
+                            nullptr, dD, dC, rocsparse_datatype_f64_r, rocsparse_spgemm_alg_default,
+                            rocsparse_spgemm_stage_compute, &bsz, buf));
+        HC(hipDeviceSynchronize());
+        double t = now_ms() - t0;
+        if (it >= 0) { sum_r += t; if (t < best_r) best_r = t; }
+    }
+
+    // ---- compare
+    bool same_nnz = nnz_e == nnz_r;
+    int64_t col_mis = 0, unsorted_e = 0, unsorted_r = 0; double max_rel = 0;
+    if (same_nnz) {
+        std::vector<int64_t> pe(n + 1), pr(n + 1);
+        std::vector<int32_t> ce(nnz_e), cr(nnz_e);
+        std::vector<double> ve(nnz_e), vr(nnz_e);
+        HC(hipMemcpy(pe.data(), Ce.row_ptr, (n + 1) * 8, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(pr.data(), rp_r, (n + 1) * 8, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(ce.data(), Ce.col, nnz_e * 4, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(cr.data(), col_r, nnz_e * 4, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(ve.data(), Ce.val, nnz_e * 8, hipMemcpyDeviceToHost));
+        HC(hipMemcpy(vr.data(), val_r, nnz_e * 8, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i <= n; ++i) col_mis += pe[i] != pr[i];
+        for (int64_t i = 0; i < n; ++i) {
+            bool se = true, sr = true;
+            for (int64_t k = pr[i] + 1; k < pr[i + 1]; ++k) {
+                se = se && ce[k - 1] < ce[k];
+                sr = sr && cr[k - 1] < cr[k];
+            }
+            unsorted_e += !se; unsorted_r += !sr;
+            if (!sr) {  // compare as per-row (column, value) sets
+                std::vector<std::pair<int32_t, double>> a, b;
+                for (int64_t k = pr[i]; k < pr[i + 1]; ++k) {
+                    a.push_back({ce[k], ve[k]}); b.push_back({cr[k], vr[k]});
+                }
+                std::sort(a.begin(), a.end()); std::sort(b.begin(), b.end());
+                for (size_t k = 0; k < a.size(); ++k) {
+                    ce[pr[i] + k] = a[k].first; ve[pr[i] + k] = a[k].second;
+                    cr[pr[i] + k] = b[k].first; vr[pr[i] + k] = b[k].second;
+                }
+            }
+        }
+        for (int64_t k = 0; k < nnz_e; ++k) {
+            col_mis += ce[k] != cr[k];
+            double d = std::fabs(ve[k] - vr[k]) / std::fmax(1.0, std::fabs(vr[k]));
+            if (d > max_rel) max_rel = d;
+        }
+    }
+    const double ge = 2.0 * flops / (best_e * 1e6), gr = 2.0 * flops / (best_r * 1e6);
+    printf("{\"workload\": \"rmat%d_ef20_seed2 A*A fp64\", \"flops\": %lld, "
+           "\"engine\": {\"nnz_c\": %lld, \"ms_best\": %.3f, \"ms_mean\": %.3f, \"gflops\": %.2f, \"ms_best_reference_order\": %.3f, \"unsorted_rows\": %lld}, "
+           "\"rocsparse\": {\"nnz_c\": %lld, \"ms_best\": %.3f, \"ms_mean\": %.3f, \"gflops\": %.2f, \"buffer_bytes\": %zu, \"unsorted_rows\": %lld}, "
+           "\"speedup_reference_order\": %.2f, \"same_nnz\": %s, \"index_mismatches\": %lld, \"max_rel_val_diff\": %.3e}\n",
+           scale, (long long)flops, (long long)nnz_e, best_e, sum_e / steps, ge, best_eref, (long long)unsorted_e,
+           (long long)nnz_r, best_r, sum_r / steps, gr, bsz, (long long)unsorted_r, best_r / best_eref,
+           same_nnz ? "true" : "false", (long long)col_mis, max_rel);
+    int ok = same_nnz && col_mis == 0 && max_rel <= 1e-12;
+    printf("%s\n", ok ? "MATCH" : "MISMATCH");
+    return ok ? 0 : 1;
+}
