@@ -1135,12 +1135,20 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const RowRef *list, int3
     int64_t o = 0;
     int32_t n = 0;
     if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
-    for (int e = lane; e < CAP; e += TEAM) {
-        sk[team][e] = e < n ? col[o + e] : INT32_MAX;
-        sv[team][e] = e < n ? val[o + e] : 0.0;
+    // A workgroup-sized team sorts only the next power of two above its row
+    // (the bins are 4x wide, so a fixed CAP sorted up to 4x the row); teams
+    // sharing a wave keep CAP so their loop trips stay uniform.
+    uint32_t cap = CAP;
+    if constexpr (TPW == 1) {
+        cap = 2;
+        while (cap < (uint32_t)n) cap <<= 1;
+    }
+    for (uint32_t e = lane; e < cap; e += TEAM) {
+        sk[team][e] = e < (uint32_t)n ? col[o + e] : INT32_MAX;
+        sv[team][e] = e < (uint32_t)n ? val[o + e] : 0.0;
     }
     Team<TEAM>::sync();
-    bitonic<TEAM>(sk[team], sv[team], CAP);
+    bitonic<TEAM>(sk[team], sv[team], cap);
     for (int e = lane; e < n; e += TEAM) {
         col[o + e] = sk[team][e];
         val[o + e] = sv[team][e];
