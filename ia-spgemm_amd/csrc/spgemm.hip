@@ -2,6 +2,7 @@
 // (replaces CSR_MUL_CSR / COO_MUL_COO / ELL_MUL_ELL of the reference and the
 // CUSP / cuSPARSE calls of GPU/main.cu:467-523).  See spgemm_kernels.hpp for
 // the per-row algorithm and DESIGN.md §4 for the pipeline and its roofline.
+#include <hipcub/hipcub.hpp>
 #include "spgemm_kernels.hpp"
 #include "onepass_kernels.hpp"
 #include "spgemm_engine.hpp"
@@ -1181,6 +1182,36 @@ __global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_
     }
 }
 
+// Rows beyond the LDS bins: gathered into a compact workspace (their binning
+// slots), sorted there by one segmented radix sort over all of them (every
+// workgroup of the chip works on them, not one per row), scattered back.
+__global__ __launch_bounds__(256) void k_wide_gather(const RowRef *list, int32_t count,
+                                                     const int64_t *ws_off, const int64_t *ptr,
+                                                     const int32_t *len, int64_t stride,
+                                                     const int32_t *col, const double *val,
+                                                     int32_t *kin, double *vin, int64_t *beg,
+                                                     int64_t *end, bool back) {
+    const int64_t idx = blockIdx.x;
+    if (idx >= count) return;
+    int64_t o;
+    int32_t n;
+    sort_row_span(ptr, len, stride, list[idx].row, o, n);
+    const int64_t w = ws_off[idx];
+    if (!back && blockIdx.y == 0 && threadIdx.x == 0) {
+        beg[idx] = w;
+        end[idx] = w + n;
+    }
+    for (int64_t e = (int64_t)blockIdx.y * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.y * 256) {
+        if (back) {
+            ((int32_t *)col)[o + e] = kin[w + e];
+            ((double *)val)[o + e] = vin[w + e];
+        } else {
+            kin[w + e] = col[o + e];
+            vin[w + e] = val[o + e];
+        }
+    }
+}
+
 __global__ void k_row_len(const int64_t *ptr, int64_t rows, int32_t *len) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < rows) len[i] = (int32_t)(ptr[i + 1] - ptr[i]);
@@ -2109,8 +2140,19 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const int wide = spec.nval + 2;
-    if (hc.count[wide] > 0)
+    const int32_t nwide = hc.count[wide];
+    const bool radix = nwide > 0 && hc.ws_slots < (unsigned long long)INT32_MAX;
+    size_t rtmp = 0;
+    const size_t slots = (size_t)hc.ws_slots;
+    if (radix) {
+        HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(
+            nullptr, rtmp, (const int32_t *)nullptr, (int32_t *)nullptr, (const double *)nullptr,
+            (double *)nullptr, (int)slots, nwide, (const int64_t *)nullptr, (const int64_t *)nullptr,
+            0, 31, s));
+        IAS_TRY(plan->reserve(ias_plan::B_TMP4, 24ull * slots + 16ull * nwide + rtmp + 256));
+    } else if (nwide > 0) {
         IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
+    }
     int64_t st[MAX_BINS];
     bin_starts(hc, st);
     auto lst = [&](int b) { return lists + st[b]; };
@@ -2127,9 +2169,28 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
         k_sort_lds<1024, 4096, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
     if ((c = hc.count[6]) > 0)
         k_sort_lds<1024, 8192, 1><<<c, 1024, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
-    if ((c = hc.count[wide]) > 0)
+    if ((c = nwide) > 0 && radix) {
+        char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
+        double *vin = (double *)b;
+        double *vout = vin + slots;
+        int64_t *beg = (int64_t *)(vout + slots);
+        int64_t *end = beg + c;
+        int32_t *kin = (int32_t *)(end + c);
+        int32_t *kout = kin + slots;
+        void *tmp = (void *)(((uintptr_t)(kout + slots) + 255) & ~(uintptr_t)255);
+        const dim3 g(c, 16);
+        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val, kin, vin, beg,
+                                        end, false);
+        HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, rtmp, (const int32_t *)kin, kout,
+                                                         (const double *)vin, vout, (int)slots, c,
+                                                         (const int64_t *)beg, (const int64_t *)end,
+                                                         0, 31, s));
+        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val, kout, vout,
+                                        beg, end, true);
+    } else if (c > 0) {
         k_sort_global<<<c, 1024, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val,
                                          (char *)plan->bufs[ias_plan::B_TMP4].p);
+    }
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
 }
