@@ -2127,7 +2127,13 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     const int32_t u[] = {0, 32, 128, 512, 2048, 4096, 8192};
     for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
-    spec.wide_min = 8193;   // everything beyond the LDS bins -> global workspace
+    // rows longer than this -> segmented radix sort (IAS_SORT_WIDE_MIN: A/B knob)
+    static const int32_t wide_min_env = [] {
+        const char *e = getenv("IAS_SORT_WIDE_MIN");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v <= 8193 ? (int32_t)v : 2049;   // 8193 / 2049 / 513 / 129: 78 / 72 / 77 / 94 ms (K3' sorted)
+    }();
+    spec.wide_min = wide_min_env;
     RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
     // the scatter's row extents are not used by the sort kernels (they read ptr/len)
