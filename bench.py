@@ -231,28 +231,32 @@ def main():
     gflops = 2.0 * flops_total / (ms_step * 1e6)
     nnz_c_total = int(nnz_tot.item())
 
-    # Roofline (HBM-bound).  Dominant launch: k_onepass, the
-    # chunk launch of the single pass (k_numeric_flat for --engine twophase),
-    # event-timed on its own stream inside the library.  Its algorithmic bytes
-    # per launch: per product the B column (4 B) and B value (8 B) gathered,
-    # per C entry 12 B written.  The whole step's B_alg = bytes(A) + bytes(B)
-    # + bytes(C) over the step time is reported beside it.
+    # Roofline (HBM-bound).  Dominant launch: k_numeric_flat
+    # (k_onepass for --engine onepass), event-timed on its own stream inside
+    # the library.  Its algorithmic bytes per launch follow §8(d3)'s B_alg:
+    # the C entries it writes (12 B each) plus one read of A and of B
+    # (bytes(X) = 8·(rows+1) + 12·nnz(X)); the B-row re-reads (12 B per
+    # product, mostly served by L2 / the Infinity Cache) are reported
+    # separately as gather_bytes, never in `achieved`.
     rows_local = r1 - r0
     bytes_a = 8 * (rows_local + 1) + 12 * int(Am.nnz)
     bytes_b = 8 * (rows + 1) + 12 * nnz_a
     bytes_c = 8 * (rows_local + 1) + 12 * local_nnz
     alg_bytes = bytes_a + bytes_b + bytes_c
     ms_flat = statistics.mean(x[4] for x in reps)
-    flat_bytes = 12 * int(rep.stream_products) + 12 * int(rep.stream_nnz)
+    flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
+    gather_bytes = 12 * int(rep.stream_products)
     achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
     kname = "k_onepass" if args.engine == "onepass" else "k_numeric_flat"
-    traffic = None
+    traffic, lds_conf = None, None
     pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
     if os.path.exists(pmc_file):
         try:
-            traffic = json.load(open(pmc_file)).get(kname, {}).get("hbm_bytes_per_launch")
+            prof = json.load(open(pmc_file))
+            traffic = prof.get(kname, {}).get("hbm_bytes_per_launch")
+            lds_conf = prof.get("lds_bank_conflict_ratio")
         except Exception:
-            traffic = None
+            traffic, lds_conf = None, None
 
     out = {
         "metric": METRIC,
@@ -291,6 +295,9 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             "alg_bytes_per_launch": flat_bytes,
+            "alg_bytes_formula": "12*c_entries + bytes(A) + bytes(B), bytes(X) = 8*(rows+1) + 12*nnz(X)",
+            "gather_bytes": gather_bytes,
+            "lds_bank_conflict_ratio": lds_conf,
             "ms_per_launch": round(ms_flat, 4),
             "units_per_launch": {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)},
         },
@@ -317,6 +324,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
         if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
             out["speedup_vs_cpu_baseline"] = round(gflops / out["cpu_baseline"]["value"], 2)
+        out["cpu_baseline_alg2"] = cpu_baseline_alg2(A, flops_total, args.cpu_threads)
 
     if rank == 0 and world == 1 and args.as_rank is None and not args.no_host_e2e:
         # the end-to-end rate with host operands (A, B uploaded, C
@@ -347,30 +355,89 @@ def main():
         dist.destroy_process_group()
 
 
+def row_sample(A, every):
+    """Every `every`-th block of 4096 rows of A (spread over the matrix, hub rows
+    included), as one CSR: the bounded sample the CPU baselines run when the
+    full product is beyond the budget (or beyond MKL LP64's 2^31 entries)."""
+    import ias
+    if every <= 1:
+        return A
+    blocks = [(r, min(r + 4096, A.rows)) for r in range(0, A.rows, 4096 * every)]
+    rp = [np.zeros(1, np.int64)]
+    cols, vals, base = [], [], 0
+    for r0, r1 in blocks:
+        s, e = int(A.row_ptr[r0]), int(A.row_ptr[r1])
+        rp.append(A.row_ptr[r0 + 1:r1 + 1] - s + base)
+        cols.append(A.col[s:e])
+        vals.append(A.val[s:e])
+        base += e - s
+    return ias.HostCsr(sum(r1 - r0 for r0, r1 in blocks), A.cols, np.concatenate(rp),
+                       np.concatenate(cols), np.concatenate(vals))
+
+
 def cpu_baseline(A, flops_total, threads):
     """The reference's Algorithm 1 (MKL mkl_sparse_sp2m, create+multiply+export
-    as main.cpp:746-748) on the host cores: 1 warm-up + median of 3 full runs."""
+    as main.cpp:746-748) on the host cores: 1 warm-up + median of 3 runs.  The
+    full matrix when its product is small enough for a bounded run; otherwise
+    a row sample (row_sample) times B = A, reported per its own flops."""
     import ias
     ok, ver = ias.mkl_available()
     if not ok:
         return {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "reference",
                 "sample": "MKL runtime not present on this host"}
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    every = 1 if flops_total <= 1_200_000_000 else int(math.ceil(flops_total / 3e8))
+    As = row_sample(A, every)
+    f_s = ias.flops(As, A)
     times = []
-    sa = A.struct()
+    sa, sb = As.struct(), A.struct()
     for i in range(4):
         cm, ms = ias.Csr(), C.c_double(0)
-        ias.check(ias.lib.ias_mkl_sp2m(C.byref(sa), C.byref(sa), C.byref(cm), threads, C.byref(ms)),
+        ias.check(ias.lib.ias_mkl_sp2m(C.byref(sa), C.byref(sb), C.byref(cm), threads, C.byref(ms)),
                   "ias_mkl_sp2m")
         ias.lib.ias_csr_free(C.byref(cm))
         if i:
             times.append(ms.value)
     med = statistics.median(times)
-    return {"value": round(2.0 * flops_total / (med * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
+    what = "full matrix" if every == 1 else \
+        f"row sample: every {every}th block of 4096 rows ({As.rows} rows, {f_s} of {flops_total} flops) x full B"
+    return {"value": round(2.0 * f_s / (med * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
             "kind": "reference",
-            "sample": f"full matrix, MKL mkl_sparse_sp2m FULL_MULT (reference Algorithm 1, "
+            "sample": f"{what}, MKL mkl_sparse_sp2m FULL_MULT (reference Algorithm 1, "
                       f"csr/common_csr.h:18-47), {ver.split(' Product')[0]}, LP64, GNU threading, "
                       f"median of 3 after 1 warm-up: {med:.1f} ms",
+            "ms": round(med, 2)}
+
+
+def cpu_baseline_alg2(A, flops_total, threads):
+    """The reference's Algorithm 2 (CSR_MUL_CSR, csr/common_csr.h:85-193: per-
+    thread dense SPA, two passes, OpenMP over rows) as restated by the oracle
+    (oracle/ias_oracle.c, the test-infrastructure CPU port; used here only as
+    the timed CPU baseline), on `threads` host threads: 1 warm-up + median of 3."""
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    try:
+        import oracle_bind as ob
+    except Exception as e:  # oracle not built on this host
+        return {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    every = 1 if flops_total <= 1_000_000_000 else int(math.ceil(flops_total / 2.5e8))
+    As = row_sample(A, every)
+    import ias
+    f_s = ias.flops(As, A)
+    Ma, Mb = ob.Mat.of(As), ob.Mat.of(A)
+    times = []
+    for i in range(4):
+        t = time.perf_counter()
+        c = ob.csr_mul_csr(Ma, Mb)
+        times.append((time.perf_counter() - t) * 1e3)
+        del c
+    med = statistics.median(times[1:])
+    what = "full matrix" if every == 1 else \
+        f"row sample: every {every}th block of 4096 rows ({f_s} of {flops_total} flops) x full B"
+    return {"value": round(2.0 * f_s / (med * 1e6), 4), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"{what}; reference Algorithm 2 CSR_MUL_CSR semantics (OpenMP restatement, "
+                      f"oracle/ias_oracle.c ora_csr_mul_csr, incl. copy-out to numpy), median of 3 after "
+                      f"1 warm-up: {med:.1f} ms",
             "ms": round(med, 2)}
 
 

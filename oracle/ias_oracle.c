@@ -201,6 +201,56 @@ void ora_csr_mul_csr(const ora_csr *A, const ora_csr *B, ora_csr *C) {
     free(cnt);
 }
 
+/* ------------------------------------------------------------------ digest
+ * CSR_MUL_CSR (csr:85-193) at sizes whose C does not fit host memory (K3:
+ * 2.28e9 entries): each row is formed exactly as gustavson_numeric forms it
+ * (reverse discovery order, sums from 0.0 in product order) and folded into
+ * an order-sensitive digest instead of being stored.  row_nnz[i] = nnz of row
+ * i; digest = sum over entries of ora_mix(row, position in row, column, value
+ * bits) mod 2^64 (addition commutes, so the thread split does not matter).
+ * tests/fulldigest.py computes the same sum on the GPU's C. */
+static inline uint64_t ora_mix(uint64_t row, uint64_t pos, uint64_t col, uint64_t vbits) {
+    uint64_t x = vbits ^ (col * 0x9E3779B97F4A7C15ull) ^ (pos * 0xC2B2AE3D27D4EB4Full) ^
+                 (row * 0x165667B19E3779F9ull);
+    x *= 0xD6E8FEB86659FD93ull;
+    return x ^ (x >> 32);
+}
+
+void ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest) {
+    const int64_t cols = B->cols;
+    uint64_t total = 0;
+#pragma omp parallel reduction(+ : total)
+    {
+        double *acc = (double *)malloc((size_t)(cols ? cols : 1) * sizeof(double));
+        char *seen = (char *)calloc((size_t)(cols ? cols : 1), 1);
+        int32_t *disc = (int32_t *)malloc((size_t)(cols ? cols : 1) * sizeof(int32_t));
+#pragma omp for schedule(dynamic, 64)
+        for (int64_t i = 0; i < A->rows; ++i) {
+            int64_t nd = 0;
+            for (int64_t p = A->row_ptr[i]; p < A->row_ptr[i + 1]; ++p) {
+                const double av = A->val[p];
+                const int32_t j = A->col[p];
+                for (int64_t q = B->row_ptr[j]; q < B->row_ptr[j + 1]; ++q) {
+                    const int32_t k = B->col[q];
+                    const double prod = av * B->val[q];
+                    if (!seen[k]) { seen[k] = 1; disc[nd++] = k; acc[k] = 0.0 + prod; }
+                    else acc[k] = acc[k] + prod;
+                }
+            }
+            for (int64_t t = 0; t < nd; ++t) {
+                const int32_t k = disc[nd - 1 - t];
+                uint64_t vb;
+                memcpy(&vb, &acc[k], sizeof vb);
+                total += ora_mix((uint64_t)i, (uint64_t)t, (uint64_t)(uint32_t)k, vb);
+                seen[k] = 0;
+            }
+            row_nnz[i] = nd;
+        }
+        free(acc); free(seen); free(disc);
+    }
+    *digest = total;
+}
+
 /* ------------------------------------------------------------------ sizes */
 double ora_sizeof_csr(const ora_csr *A) { return 4.0 * (double)(A->rows + 1 + A->nnz + 3) + 8.0 * (double)A->nnz; }
 double ora_sizeof_coo(const ora_coo *A) { return 4.0 * (double)(A->rows + 1 + 2 * A->nnz + 3) + 8.0 * (double)A->nnz; }

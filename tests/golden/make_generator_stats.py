@@ -1,10 +1,16 @@
 """Records the exact statistics of the deterministic generators
 (ia-spgemm_amd/csrc/gen.cpp) into generator_stats.json; tests/test_generators.py
-checks the library still produces them.  nnz(C) comes from the oracle."""
+checks the library still produces them.  nnz(C), the sha256 of C's row
+pointer and the order-sensitive digest of C (tests/fulldigest.py) come from
+the oracle's CSR_MUL_CSR restatement, folded row by row
+(ora_csr_mul_csr_digest), so the full-size configurations K1-K3 and K3'
+ are pinned even where C does not fit host memory; the GPU
+tests (tests/test_fullsize.py) compare the engine's C against these."""
 import hashlib
 import json
 import os
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "ia-spgemm_amd"))
@@ -17,7 +23,11 @@ CASES = {
     "rmat14_ef20_s2_int": ("rmat", (14, 20.0, 0.45, 0.15, 0.15, 2, 1)),
     "band4096_h3_s7": ("band", (4096, 3, 7, 0)),
     "ell8192_k16_s7": ("ell", (8192, 16, 7, 0)),
+    # the BASELINE.json configurations at full size
+    "k1_band262144_h3_s7": ("band", (1 << 18, 3, 7, 0)),
+    "k2_ell1048576_k16_s7": ("ell", (1 << 20, 16, 7, 0)),
     "k3p_rmat20_ef20_s2": ("rmat", (20, 20.0, 0.45, 0.15, 0.15, 2, 0)),
+    "k3_rmat20_ef32_s1": ("rmat", (20, 32.0, 0.45, 0.15, 0.15, 1, 0)),
 }
 
 
@@ -33,14 +43,21 @@ def digest(A):
 
 
 if __name__ == "__main__":
-    out = {}
+    only = set(sys.argv[1:])
+    path = os.path.join(HERE, "generator_stats.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
     for name, (kind, args) in CASES.items():
+        if only and name not in only:
+            continue
+        t = time.time()
         A = make(kind, args)
         rec = {"kind": kind, "args": list(args), "rows": A.rows, "nnz": A.nnz,
                "flops": ias.flops(A, A), "sha256": digest(A)}
-        if A.nnz < 5_000_000:
-            rec["nnz_c"] = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A)).nnz
+        rp, dg = ob.csr_mul_csr_digest(ob.Mat.of(A), ob.Mat.of(A))
+        rec["nnz_c"] = int(rp[-1])
+        rec["c_row_ptr_sha256"] = hashlib.sha256(rp.tobytes()).hexdigest()
+        rec["c_digest"] = dg
         out[name] = rec
-        print(name, rec)
-    with open(os.path.join(HERE, "generator_stats.json"), "w") as f:
-        json.dump(out, f, indent=1)
+        print(name, rec, f"{time.time() - t:.1f}s", flush=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)

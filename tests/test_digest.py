@@ -1,0 +1,42 @@
+"""The full-size digest (tests/fulldigest.py) agrees with the oracle's
+streaming digest (ora_csr_mul_csr_digest) on products small enough to
+materialise, and its torch form (run on the GPU's C by test_fullsize.py)
+agrees with the numpy form — so a digest match at full size means C matches
+the oracle entry for entry."""
+import numpy as np
+import pytest
+
+import ias
+import oracle_bind as ob
+from fulldigest import digest_numpy, digest_torch
+
+
+@pytest.mark.parametrize("A", [ias.gen_rmat(12, 16, seed=1), ias.gen_band(4096, 3, seed=7),
+                               ias.gen_ell(8192, 16, seed=7), ias.gen_rmat(11, 8, seed=4, value_mode=1)],
+                         ids=["rmat12", "band4k", "ell8k", "rmat11_int"])
+def test_digest_matches_materialised_oracle(A):
+    M = ob.Mat.of(A)
+    ref = ob.csr_mul_csr(M, M)
+    rp, dg = ob.csr_mul_csr_digest(M, M)
+    np.testing.assert_array_equal(rp, ref.row_ptr)
+    assert digest_numpy(ref.row_ptr, ref.col, ref.val) == dg
+    # order and value bits matter: swapping two entries of a row, or one ulp, changes it
+    i = int(np.argmax(np.diff(ref.row_ptr) >= 2))
+    s = int(ref.row_ptr[i])
+    col2 = ref.col.copy()
+    col2[s], col2[s + 1] = col2[s + 1], col2[s]
+    assert digest_numpy(ref.row_ptr, col2, ref.val) != dg
+    val2 = ref.val.copy()
+    val2[s] = np.nextafter(val2[s], np.inf)
+    assert digest_numpy(ref.row_ptr, ref.col, val2) != dg
+
+
+def test_torch_digest_equals_numpy():
+    torch = pytest.importorskip("torch")
+    A = ias.gen_rmat(12, 16, seed=1)
+    M = ob.Mat.of(A)
+    ref = ob.csr_mul_csr(M, M)
+    want = digest_numpy(ref.row_ptr, ref.col, ref.val)
+    got = digest_torch(torch.from_numpy(ref.row_ptr), torch.from_numpy(ref.col), torch.from_numpy(ref.val),
+                       chunk=100_000)
+    assert got == want
