@@ -5,6 +5,7 @@
 #include <hipcub/hipcub.hpp>
 #include "spgemm_kernels.hpp"
 #include "onepass_kernels.hpp"
+#include "sym2_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
 
@@ -28,7 +29,7 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
 
 // stv: the row's streaming state (-2: none given; >= 0: a streaming row with
 // stv duplicates -> the fix-up bin when it has any, nothing to do otherwise).
-__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv) {
+__device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv, int32_t ent2 = 0) {
     if (k <= 0) return 0;
     if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), longer (sorted)
         if (stv == 0) return 0;
@@ -39,7 +40,7 @@ __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod
         sp.ratio_den == 0 || (int64_t)prod * sp.ratio_den > (int64_t)k * sp.ratio_num;
     if (val_class)
         for (int i = 1; i <= sp.nval; ++i)
-            if (k <= sp.upper[i]) return i;
+            if (k <= sp.upper[i] && ent2 <= sp.upper[i]) return i;
     for (int i = 0; i < sp.ndw; ++i)
         if (k <= sp.upper[sp.nval + 3 + i]) return sp.nval + 3 + i;
     return sp.nval + 1;
@@ -208,8 +209,16 @@ constexpr int BIN_BLOCK = 256;
 constexpr int BIN_RPT = 8;                       // rows per thread of the row passes
 constexpr int BIN_ROWS = BIN_BLOCK * BIN_RPT;    // rows per block
 
+__device__ __forceinline__ int32_t ent2_of(const BinSpec &sp, const Rows &A, int64_t r) {
+    if (!sp.ent_key) return 0;
+    int64_t s;
+    int32_t n;
+    A.row(r, s, n);
+    return n > INT32_MAX / sp.ent_key ? INT32_MAX : sp.ent_key * n;
+}
+
 __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int64_t rows, int32_t *prod,
-                                                       BinSpec spec, Counters *cnt) {
+                                                       BinSpec spec, Counters *cnt, Rows A) {
     int b[BIN_RPT];
     int32_t k[BIN_RPT];
     int mx = 0;
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
             const int64_t p = poff[r + 1] - poff[r];
             k[i] = (int32_t)min(p, (int64_t)INT32_MAX);
             prod[r] = k[i];
-            b[i] = bin_of(spec, k[i], k[i], -2);
+            b[i] = bin_of(spec, k[i], k[i], -2, ent2_of(spec, A, r));
             mx = max(mx, k[i]);
         }
     }
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
                                                            int64_t *ws_off, int64_t *dup_off,
                                                            int32_t *dupn, int32_t *nnz_row,
                                                            const int64_t *qstart, Counters *cnt,
-                                                           int64_t *pfirst, int64_t *pboff) {
+                                                           int64_t *pfirst, int64_t *pboff, int sym2) {
     __shared__ int hist[MAX_BINS];
     __shared__ int64_t base[MAX_BINS];
     __shared__ int64_t bin_start[MAX_BINS];
@@ -331,7 +340,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         k[i] = 0;
         if (r < rows) {
             k[i] = key[r];
-            b[i] = bin_of(spec, k[i], prod ? prod[r] : k[i], stn ? stn[r] : -2);
+            b[i] = bin_of(spec, k[i], prod ? prod[r] : k[i], stn ? stn[r] : -2, ent2_of(spec, A, r));
             if (b[i] == 0 && spec.zero_nnz) nnz_row[r] = 0;
             if (b[i] == 0 && dupn) dupn[r] = 0;
             if (b[i] > 0) local[i] = atomicAdd(&hist[b[i]], 1);
@@ -362,7 +371,19 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
         const int64_t within = base[b[i]] + local[i];
         RowRef ref;
         ref.row = (int32_t)r;
-        if (qstart) {   // products of the row in the expansion
+        if (sym2) {     // sym2 bins: the row's A entries; partitioned rows: their products in the
+                        // compact expansion of the partitioned rows (at the bucket offset)
+            if (b[i] == part_bin) {
+                ref.q0 = (int64_t)at[4];
+                ref.n = k[i];
+            } else {
+                int64_t s;
+                int32_t nn;
+                A.row(r, s, nn);
+                ref.q0 = s - A.base();
+                ref.n = nn;
+            }
+        } else if (qstart) {   // products of the row in the expansion
             ref.q0 = qstart[r];
             ref.n = k[i];
         } else {        // entries of the row in the expanded A
@@ -1212,6 +1233,29 @@ __global__ __launch_bounds__(256) void k_wide_gather(const RowRef *list, int32_t
     }
 }
 
+// Compact expansion of the partitioned rows only (sym2): the product columns
+// of each listed row at tcol[ref.q0 + p] (ref.q0 = the row's offset in the
+// compact space), for the partition bucketing; the LDS-bin rows gather their
+// columns from B themselves.  Workgroups (row, y) take the row's A entries
+// y*4 + wave, y*4 + wave + 4*gridDim.y, ...; lanes over the entry's B row.
+__global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const int64_t *axp, const int64_t *poff,
+                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol) {
+    const RowRef ref = list[blockIdx.x];
+    int64_t s;
+    int32_t n;
+    A.row(ref.row, s, n);
+    const int64_t q0 = s - A.base();
+    const int64_t p0 = poff[ref.row];
+    const int w = (int)(threadIdx.x / WAVE), lane = (int)(threadIdx.x & (WAVE - 1));
+    for (int32_t e = (int32_t)blockIdx.y * 4 + w; e < n; e += 4 * (int32_t)gridDim.y) {
+        const int64_t q = q0 + e;
+        const int32_t bl = ax.blen[q];
+        const int64_t bs = ax.bstart[q];
+        int32_t *dst = tcol + ref.q0 + (axp[q] - p0);
+        for (int32_t j = lane; j < bl; j += WAVE) dst[j] = bcol[bs + j];
+    }
+}
+
 __global__ void k_row_len(const int64_t *ptr, int64_t rows, int32_t *len) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < rows) len[i] = (int32_t)(ptr[i + 1] - ptr[i]);
@@ -1264,6 +1308,21 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
                                      {512, 4},  {768, 5},  {1024, 5}, {1536, 6},  {2048, 6},
                                      {3072, 7}, {4096, 7}, {6144, 7}, {8192, 7},  {DW_MAX, 7}};
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
+// sym2 (sym2_kernels.hpp, the default): rows up to SYM2_MAX products whose
+// entry count fits (2 * entries <= bound) gather from B; the rest are
+// hash-partitioned.  cfg: 0..3 = one-wave teams (K = 1, 2, 4, 8 products per
+// lane, 4 teams per workgroup), 4..7 = 128..1024-lane teams with K = 8.
+constexpr int32_t SYM2_MAX = 8192;
+static constexpr BinCfg SYM2_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {768, 4},  {1024, 4},
+                                       {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6}, {6144, 7}, {SYM2_MAX, 7}};
+constexpr int N_SYM2 = sizeof(SYM2_BINS) / sizeof(SYM2_BINS[0]);
+static bool sym2_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SYM2");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
 static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
@@ -1304,11 +1363,20 @@ static_assert(val_bins_covered(), "value-bin emission does not cover a bin's tab
 
 static BinSpec sym_spec() {
     BinSpec s{};
-    s.nval = N_SYM;
     s.ndw = 0;
-    for (int i = 0; i < N_SYM; ++i) {
-        s.upper[i + 1] = SYM_BINS[i].upper;
-        s.dcap[i + 1] = dcap_for(SYM_BINS[i].upper);
+    if (sym2_on()) {
+        s.nval = N_SYM2;
+        for (int i = 0; i < N_SYM2; ++i) {
+            s.upper[i + 1] = SYM2_BINS[i].upper;
+            s.dcap[i + 1] = dcap_for(SYM2_BINS[i].upper);
+        }
+        s.ent_key = 4;   // the row's non-empty entries are staged in LDS, upper/4 of them
+    } else {
+        s.nval = N_SYM;
+        for (int i = 0; i < N_SYM; ++i) {
+            s.upper[i + 1] = SYM_BINS[i].upper;
+            s.dcap[i + 1] = dcap_for(SYM_BINS[i].upper);
+        }
     }
     s.ratio_num = 0;
     s.ratio_den = 0;
@@ -1447,6 +1515,32 @@ static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, u
         case 5: sym_launch<256, SYM_K5, 1, 1>(l, tcol, W, D, nnz, a); break;
         case 6: sym_launch<512, SYM_K6, 1, 1>(l, tcol, W, D, nnz, a); break;
         default: sym_launch<1024, SYM_K7, 1, 1>(l, tcol, W, D, nnz, a); break;
+    }
+}
+
+static Sym2Layout sym2_layout(int32_t upper) { return Sym2Layout::for_bound((uint32_t)upper); }
+
+template <int TEAM, int K, int TPW>
+static void sym2_launch(Sym2Args a, hipStream_t s) {
+    auto kern = k_sym2<TEAM, K, TPW>;
+    static bool done = false;
+    const size_t lds = (size_t)TPW * a.lay.bytes();
+    allow_lds(kern, done, lds);
+    int64_t grid = grid_for(a.count, TPW);
+    grid = std::min<int64_t>(grid, resident_blocks(kern, TEAM * TPW, lds));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), TEAM * TPW, lds, s>>>(a);
+}
+
+static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
+    switch (cfg) {
+        case 0: sym2_launch<64, 1, 4>(a, s); break;
+        case 1: sym2_launch<64, 2, 4>(a, s); break;
+        case 2: sym2_launch<64, 4, 4>(a, s); break;
+        case 3: sym2_launch<64, 8, 4>(a, s); break;
+        case 4: sym2_launch<128, 8, 1>(a, s); break;
+        case 5: sym2_launch<256, 8, 1>(a, s); break;
+        case 6: sym2_launch<512, 8, 1>(a, s); break;
+        default: sym2_launch<1024, 8, 1>(a, s); break;
     }
 }
 
@@ -1675,7 +1769,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     }
     k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff);
     if (rows > 0)
-        k_an_rows<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc);
+        k_an_rows<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
     CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
@@ -1704,10 +1798,12 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     flops = (int64_t)c1.flops;
     max_prod = c1.max_prod;
 
-    // ---- expansion: every row's product columns, contiguous
-    IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(flops, 1)));
+    // ---- expansion: every row's product columns, contiguous (sym2: only the
+    // partitioned rows', in their compact space; the LDS bins gather from B)
+    const bool sym2 = sym2_on();
+    IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(sym2 ? (int64_t)c1.part_prod : flops, 1)));
     const int32_t *tcol = as<int32_t>(bufs[B_TCOL]);
-    if (a_entries > 0) {
+    if (a_entries > 0 && !sym2) {
         const int64_t nchunks = (a_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
         const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 4096);
         k_expand<<<grid, FLAT_BLOCK, 0, s>>>(ax, axp, a_entries, B, as<int32_t>(bufs[B_TCOL]));
@@ -1736,7 +1832,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
             as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc, as<int64_t>(bufs[B_PFIRST]),
-            as<int64_t>(bufs[B_PBOFF]));
+            as<int64_t>(bufs[B_PBOFF]), sym2 ? 1 : 0);
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
     HIPC(hipEventRecord(ev[1], s));
     int64_t st[MAX_BINS];
@@ -1747,6 +1843,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
         const bool pb = part_bucket();
+        if (sym2)
+            k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+                                                               as<int32_t>(bufs[B_TCOL]));
         if (pb)
             k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
@@ -1760,7 +1859,20 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                       sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
-    for (int b = ss.nval; b >= 1; --b)
+    for (int b = ss.nval; b >= 1 && sym2; --b)
+        if ((c = c1.count[b]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            const int32_t u = SYM2_BINS[b - 1].upper;
+            static const int abl = [] {
+                const char *e = getenv("IAS_S2_ABLATE");
+                return e ? atoi(e) : 0;
+            }();
+            Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u), nnz, bm,
+                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl};
+            sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
+            CHECK_LAUNCH("k_sym2", t);
+        }
+    for (int b = ss.nval; b >= 1 && !sym2; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
             const int32_t u = SYM_BINS[b - 1].upper;
@@ -1785,7 +1897,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
-            nullptr, dc2, nullptr, nullptr);
+            nullptr, dc2, nullptr, nullptr, 0);
     CHECK_LAUNCH("numeric binning", s);
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
@@ -2141,7 +2253,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
     k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
                                                                   lists, nullptr, nullptr, offs, nullptr,
-                                                                  nullptr, nullptr, nullptr, dc, nullptr, nullptr);
+                                                                  nullptr, nullptr, nullptr, dc, nullptr, nullptr, 0);
     Counters hc;
     HIPC(hipMemcpyAsync(&hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));

@@ -27,6 +27,8 @@ struct BinSpec {
     int32_t part_dcap_max;
     int32_t ft;                // give every listed row a first-touch bitmap
     int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
+    int32_t ent_key;           // > 0: LDS bin i also needs ent_key * (A entries of the row) <= upper[i]
+                               // (sym2 stages the row's entry bases in LDS, upper/ent_key of them)
 };
 
 // Device-side counters, copied to the host after each binning.

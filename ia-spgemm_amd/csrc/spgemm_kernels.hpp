@@ -973,7 +973,7 @@ template <int K>
 // FLAT_BCOL=1: the flat numeric reads the product's column from B itself
 // (the line it gathers the value's row from) instead of the expansion.
 #ifndef FLAT_BCOL
-#define FLAT_BCOL 0
+#define FLAT_BCOL 1   // the expansion now covers only the partitioned rows (sym2)
 #endif
 // FLAT_NT=1: C leaves through non-temporal stores (not read back; B's rows
 // keep the caches); STREAM_NT=1: the expansion is written and read the same way.

@@ -1,7 +1,5 @@
 #!/bin/bash
+# timing build + per-phase row-kernel timings (tools/timing.sh), one box call
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-tim} bash tools/timing.sh
-rc=$?
-cat gpurun_out/${TAG:-tim}/timing.txt
-exit $rc

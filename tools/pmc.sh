@@ -16,10 +16,11 @@ while read -r group; do
   rc=$?
   echo "group $i rc=$rc: $group" >> $OUT/pmc_status.txt
   case $rc in 124|134|137|139) exit $rc;; esac
-done <<'GROUPS'
+done < <(if [ -n "$PMC_GROUPS" ]; then printf '%s\n' "$PMC_GROUPS" | tr ';' '\n'; else cat <<'GROUPS'
 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
 SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS
 FETCH_SIZE
 WRITE_SIZE
 TCC_HIT_sum TCC_MISS_sum
 GROUPS
+fi)
