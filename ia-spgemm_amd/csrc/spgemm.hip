@@ -1309,10 +1309,13 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
                                      {3072, 7}, {4096, 7}, {6144, 7}, {8192, 7},  {DW_MAX, 7}};
 constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 // sym2 (sym2_kernels.hpp, the default): rows up to SYM2_MAX products whose
-// entry count fits (2 * entries <= bound) gather from B; the rest are
-// hash-partitioned.  cfg: 0..3 = one-wave teams (K = 1, 2, 4, 8 products per
-// lane, 4 teams per workgroup), 4..7 = 128..1024-lane teams with K = 8.
+// entry count fits (8 * entries <= bound) gather from B; the rest are
+// hash-partitioned.  cfg: 0..3 = one-wave teams (K = 1 .. 8 products per
+// lane, 4 teams per workgroup: no workgroup barrier per row), 4..7 = 128- to
+// 1024-lane teams with K = 8 (one-wave teams with K = 16 / 32 measured slower:
+// 160-256 VGPRs, 2-3 waves per SIMD).
 constexpr int32_t SYM2_MAX = 8192;
+constexpr int SYM2_WAVE_CFG_MAX = 3;
 static constexpr BinCfg SYM2_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {768, 4},  {1024, 4},
                                        {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6}, {6144, 7}, {SYM2_MAX, 7}};
 constexpr int N_SYM2 = sizeof(SYM2_BINS) / sizeof(SYM2_BINS[0]);
@@ -1370,7 +1373,7 @@ static BinSpec sym_spec() {
             s.upper[i + 1] = SYM2_BINS[i].upper;
             s.dcap[i + 1] = dcap_for(SYM2_BINS[i].upper);
         }
-        s.ent_key = 4;   // the row's non-empty entries are staged in LDS, upper/4 of them
+        s.ent_key = 8;   // the row's non-empty entries are staged in LDS, upper/8 of them
     } else {
         s.nval = N_SYM;
         for (int i = 0; i < N_SYM; ++i) {
@@ -1518,11 +1521,13 @@ static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, u
     }
 }
 
-static Sym2Layout sym2_layout(int32_t upper) { return Sym2Layout::for_bound((uint32_t)upper); }
+static Sym2Layout sym2_layout(int32_t upper, int cfg) {
+    return Sym2Layout::for_bound((uint32_t)upper, cfg <= SYM2_WAVE_CFG_MAX);
+}
 
-template <int TEAM, int K, int TPW>
+template <int TEAM, int K, int TPW, int WPE = 1>
 static void sym2_launch(Sym2Args a, hipStream_t s) {
-    auto kern = k_sym2<TEAM, K, TPW>;
+    auto kern = k_sym2<TEAM, K, TPW, WPE>;
     static bool done = false;
     const size_t lds = (size_t)TPW * a.lay.bytes();
     allow_lds(kern, done, lds);
@@ -1537,7 +1542,7 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
         case 1: sym2_launch<64, 2, 4>(a, s); break;
         case 2: sym2_launch<64, 4, 4>(a, s); break;
         case 3: sym2_launch<64, 8, 4>(a, s); break;
-        case 4: sym2_launch<128, 8, 1>(a, s); break;
+        case 4: sym2_launch<128, 8, 1>(a, s); break;   // one-wave K=16 measured 30 % slower
         case 5: sym2_launch<256, 8, 1>(a, s); break;
         case 6: sym2_launch<512, 8, 1>(a, s); break;
         default: sym2_launch<1024, 8, 1>(a, s); break;
@@ -1867,7 +1872,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const char *e = getenv("IAS_S2_ABLATE");
                 return e ? atoi(e) : 0;
             }();
-            Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u), nnz, bm,
+            Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
                         sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl};
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);

@@ -172,6 +172,21 @@ struct Bitmap {
     const int64_t *off;   // per row, in words
 };
 
+// ---------------------------------------------------------------- wave scan
+// Inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS
+// round trip per step, unlike __shfl_up = ds_bpermute): row_shr 1/2/4/8 scan
+// each 16-lane row, row_bcast:15 / row_bcast:31 carry across rows (GFX9 DPP,
+// gfx950).  Inactive source lanes read as 0 (old = 0).
+__device__ __forceinline__ int wave_incl_sum(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 // ---------------------------------------------------------------- team ops
 // A team is TEAM consecutive lanes.  TEAM <= 64: several teams per wave,
 // synchronised at wave level.  TEAM > 64: exactly one team per workgroup.
@@ -205,13 +220,17 @@ struct Team {
         constexpr int W = MULTI ? WAVE : TEAM;
         const int l = (int)(threadIdx.x & (W - 1));
         int x = v;
+        if constexpr (W == WAVE) {
+            x = wave_incl_sum(v);
+        } else {
 #pragma unroll
-        for (int d = 1; d < W; d <<= 1) {
-            const int t = __shfl_up(x, d, W);
-            if (l >= d) x += t;
+            for (int d = 1; d < W; d <<= 1) {
+                const int t = __shfl_up(x, d, W);
+                if (l >= d) x += t;
+            }
         }
         if constexpr (!MULTI) {
-            total = __shfl(x, W - 1, W);
+            total = W == WAVE ? __builtin_amdgcn_readlane(x, WAVE - 1) : __shfl(x, W - 1, W);
             return x - v;
         } else {
             const int w = threadIdx.x / WAVE;

@@ -47,8 +47,8 @@ namespace dev {
 
 // LDS layout of one sym2 team for rows of at most U products:
 // [f1 4FW | f2 4FW | list 8LC | keys 4ES | own 4ES | ebase 8EC | mask 8W | wpre 4W | lbits 8W | lpref 8W | scratch]
-// FW = filter words (16 bits per product), LC = list capacity (U/4), ES = exact-table
-// slots (2 LC), EC = non-empty entries (U/4), W = 64-bit mask words.
+// FW = filter words (8 or 16 bits per product), LC = list capacity (U/8 or U/4), ES =
+// exact-table slots (2 LC), EC = non-empty entries (U/8), W = 64-bit mask words.
 struct Sym2Layout {
     uint32_t U, FW, LC, ES, EC, W;
     __host__ __device__ static constexpr size_t r16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -66,13 +66,16 @@ struct Sym2Layout {
     __host__ __device__ size_t bytes() const { return scratch() + 256; }
     // the heavy-row fallback's keys-only table spans f1 .. own
     __host__ __device__ uint32_t heavy_slots() const { return (uint32_t)((ebase() - f1()) / 4); }
-    __host__ static Sym2Layout for_bound(uint32_t upper) {
+    // one-wave teams (wide rows on one wave: LDS per wave is the limit) keep
+    // 8 filter bits and an eighth of the products for the exact list; the
+    // workgroup teams 16 bits and a quarter
+    __host__ static Sym2Layout for_bound(uint32_t upper, bool one_wave) {
         Sym2Layout L;
         L.U = upper;
-        L.FW = upper / 2;          // 16 bits per product
-        L.LC = upper / 4;
+        L.FW = one_wave ? upper / 4 : upper / 2;
+        L.LC = one_wave ? upper / 8 : upper / 4;
         L.ES = 2 * L.LC;
-        L.EC = upper / 4;
+        L.EC = upper / 8;
         L.W = (upper + 63) / 64;
         return L;
     }
@@ -153,12 +156,16 @@ __device__ __forceinline__ uint32_t reduce32(uint32_t h, uint32_t n) {
 }
 __device__ __forceinline__ uint32_t fib(int32_t c) { return (uint32_t)c * 0x9E3779B1u; }
 
-template <int TEAM, int K, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_sym2(Sym2Args a) {
+// WPE: minimum waves per SIMD the register allocation must allow (one-wave
+// teams with K >= 16 would otherwise take 160-256 VGPRs, 2 waves per SIMD).
+template <int TEAM, int K, int TPW, int WPE>
+__global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sym2(Sym2Args a) {
     static_assert(TEAM >= WAVE && (TEAM <= WAVE || TPW == 1), "teams are whole waves; multi-wave teams own the WG");
-    static_assert(K <= 8, "finish() covers the bitmap words in one pass, the list in K/4 passes");
+    static_assert(TEAM == WAVE ? K <= 32 : K <= 8, "finish() covers the bitmap words in one pass");
     using TM = Team<TEAM>;
-    constexpr int LPASS = K > 4 ? K / 4 : 1;   // list capacity U/4 <= LPASS * TEAM
+    constexpr int LPASS = K > 4 ? K / 4 : 1;   // list capacity <= U/4 <= LPASS * TEAM
+    constexpr int CH = K < 8 ? K : 8;          // items per register chunk
+    constexpr bool DB = K <= 8;                // next row's columns gathered during this row's work
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Sym2Layout L = a.lay;
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
@@ -234,62 +241,96 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sym2(Sym2Args a) {
     };
     // ---- gather the staged row's columns: K loads in flight per lane, not waited here
     auto gather = [&](int32_t P, int32_t (&c)[K]) __attribute__((always_inline)) {
+        // branch-free (clamped indices, a safe dummy address for items beyond
+        // P): the compiler then issues a chunk's LDS reads together and its
+        // loads back to back instead of one exec-masked block per item
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int p = k * TEAM + lane;
-            c[k] = -1;
-            if (p < P) {
-                if (a.ablate & 2) {
-                    c[k] = p;
-                } else {
-                    const unsigned long long m = mask[p >> 6];
-                    const int e = (int)wpre[p >> 6] + __popcll(m & ((2ull << (p & 63)) - 1ull)) - 1;
-                    c[k] = a.bcol[ebase[e] + p];
-                }
+        for (int k0 = 0; k0 < K; k0 += CH) {
+            int64_t at[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int p = (k0 + t) * TEAM + lane;
+                const int pc = p < P ? p : 0;
+                const unsigned long long m = mask[pc >> 6];
+                const int e = (int)wpre[pc >> 6] + __popcll(m & ((2ull << (pc & 63)) - 1ull)) - 1;
+                at[t] = ebase[e] + pc;
+            }
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int p = (k0 + t) * TEAM + lane;
+                c[k0 + t] = (a.ablate & 2) ? p : a.bcol[p < P ? at[t] : 0];
             }
         }
     };
     // ---- filter + exact resolution (steps 3-4); returns the listed count L,
     // or -1 for a heavy row (then *hcount = its distinct columns)
     auto resolve = [&](int32_t P, const int32_t (&c)[K]) __attribute__((always_inline)) -> int32_t {
-        // 3a. f1 with return; candidates mark f2
+        // 3a. f1 with return; candidates mark f2 (branch-free: items beyond P
+        // OR nothing into word 0, so a chunk's atomics issue back to back)
         uint32_t candm = 0u;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int p = k * TEAM + lane;
-            if (p < P) {
-                const uint32_t bit = reduce32(fib(c[k]), FB);
-                const uint32_t m = 1u << (bit & 31);
-                const uint32_t old = atomicOr(&f1[bit >> 5], m);
-                if (old & m) {
-                    candm |= 1u << k;
-                    atomicOr(&f2[bit >> 5], m);
-                }
+        for (int k0 = 0; k0 < K; k0 += CH) {
+            uint32_t word[CH], bitm[CH], old[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool in = (k0 + t) * TEAM + lane < P;
+                const uint32_t bit = reduce32(fib(c[k0 + t]), FB);
+                word[t] = in ? bit >> 5 : 0u;
+                bitm[t] = in ? 1u << (bit & 31) : 0u;
+            }
+#pragma unroll
+            for (int t = 0; t < CH; ++t) old[t] = atomicOr(&f1[word[t]], bitm[t]);
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool cand = (old[t] & bitm[t]) != 0u;
+                candm |= (cand ? 1u : 0u) << (k0 + t);
+                atomicOr(&f2[word[t]], cand ? bitm[t] : 0u);
             }
         }
         TM::sync();
-        // 3b. classify: certain first touches -> bitmap words; possible duplicates -> list
+        // 3b. classify: certain first touches -> bitmap words; possible
+        // duplicates -> list (one list atomic per wave and chunk)
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int p = k * TEAM + lane;
-            bool poss = false;
-            if (p < P) {
-                const uint32_t bit = reduce32(fib(c[k]), FB);
-                poss = ((candm >> k) & 1u) || ((f2[bit >> 5] >> (bit & 31)) & 1u);
+        for (int k0 = 0; k0 < K; k0 += CH) {
+            uint32_t f2w[CH], bitm[CH];
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const bool in = (k0 + t) * TEAM + lane < P;
+                const uint32_t bit = reduce32(fib(c[k0 + t]), FB);
+                bitm[t] = in ? 1u << (bit & 31) : 0u;
+                f2w[t] = f2[in ? bit >> 5 : 0u];
             }
-            const uint64_t wb = __ballot(p < P && !poss);
-            const uint32_t p0 = (uint32_t)(k * TEAM) + (uint32_t)(lane & ~(WAVE - 1));   // 64-aligned
-            if ((lane & (WAVE - 1)) == 0 && p0 < (uint32_t)P) {
-                lbits[p0 >> 5] = (uint32_t)wb;
-                lbits[(p0 >> 5) + 1] = (uint32_t)(wb >> 32);
+            uint64_t pb[CH];
+            uint32_t possm = 0u;
+            int ptot = 0;
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int k = k0 + t;
+                const int p = k * TEAM + lane;
+                const bool poss = ((candm >> k) & 1u) || (f2w[t] & bitm[t]) != 0u;
+                possm |= (poss ? 1u : 0u) << t;
+                const uint64_t wb = __ballot(p < P && !poss);
+                const uint32_t p0 = (uint32_t)(k * TEAM) + (uint32_t)(lane & ~(WAVE - 1));   // 64-aligned
+                if ((lane & (WAVE - 1)) == 0 && p0 < (uint32_t)P) {
+                    lbits[p0 >> 5] = (uint32_t)wb;
+                    lbits[(p0 >> 5) + 1] = (uint32_t)(wb >> 32);
+                }
+                pb[t] = __ballot(poss);
+                ptot += __popcll(pb[t]);
             }
-            const uint64_t pb = __ballot(poss);
-            if (pb) {
-                const int leader = __builtin_ctzll(pb);
+            if (ptot) {
                 int at = 0;
-                if ((int)__lane_id() == leader) at = atomicAdd(lcount, __popcll(pb));
-                at = __shfl(at, leader) + __popcll(pb & ((1ull << __lane_id()) - 1ull));
-                if (poss && (uint32_t)at < L.LC) list[at] = make_int2(c[k], p);
+                if (__lane_id() == 0) at = atomicAdd(lcount, ptot);
+                at = __builtin_amdgcn_readfirstlane(at);
+                const uint64_t lt = (1ull << __lane_id()) - 1ull;
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    if ((possm >> t) & 1u) {
+                        const int i = at + __popcll(pb[t] & lt);
+                        if ((uint32_t)i < L.LC) list[i] = make_int2(c[k0 + t], (k0 + t) * TEAM + lane);
+                    }
+                    at += __popcll(pb[t]);
+                }
             }
         }
         TM::sync();
@@ -404,6 +445,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sym2(Sym2Args a) {
     if (row >= 0) {
         stage(uni64(cur.ref.q0), uni(cur.ref.n), P, cur.bl, cur.bs);
         gather(P, c);
+        TM::sync();   // every wave has read the staging arrays before the loop's stage() rewrites them
     }
     Sym2Row nxt = sym2_detail<TEAM>(a, sym2_ref<TEAM>(a, idx + nteams));
     RowRef nref = sym2_ref<TEAM>(a, idx + 2 * nteams);
@@ -420,11 +462,11 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sym2(Sym2Args a) {
         __builtin_amdgcn_s_waitcnt(0x0F70);
         tm.mark(0);
         const int32_t nrow = uni(nxt.ref.row), nP = uni(nxt.P);
-        int32_t cn[K];
+        int32_t cn[DB ? K : 1];
         if (nrow >= 0) {
             stage(uni64(nxt.ref.q0), uni(nxt.ref.n), nP, nxt.bl, nxt.bs);
             tm.mark(1);
-            gather(nP, cn);
+            if constexpr (DB) gather(nP, cn);
         }
         const Sym2Row nn = sym2_detail<TEAM>(a, nref);
         nref = sym2_ref<TEAM>(a, idx + 3 * nteams);
@@ -436,8 +478,12 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sym2(Sym2Args a) {
         TM::sync();   // tables / lbits / list are the next row's
         tm.mark(6);
         tm.done();
+        if constexpr (DB) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) c[k] = cn[k];
+            for (int k = 0; k < K; ++k) c[k] = cn[(DB ? k : 0)];
+        } else if (nrow >= 0) {
+            gather(nP, c);   // one register set: other waves cover the load latency
+        }
         row = nrow;
         P = nP;
         bmoff = uni64(nxt.bmoff);
