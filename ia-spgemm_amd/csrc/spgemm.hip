@@ -1536,16 +1536,19 @@ static void sym2_launch(Sym2Args a, hipStream_t s) {
     kern<<<(unsigned)std::max<int64_t>(grid, 1), TEAM * TPW, lds, s>>>(a);
 }
 
+#ifndef SYM2_WPE_TEAM
+#define SYM2_WPE_TEAM 1   // waves per SIMD the multi-wave teams' registers must allow (1: no cap)
+#endif
 static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
     switch (cfg) {
         case 0: sym2_launch<64, 1, 4>(a, s); break;
         case 1: sym2_launch<64, 2, 4>(a, s); break;
         case 2: sym2_launch<64, 4, 4>(a, s); break;
         case 3: sym2_launch<64, 8, 4>(a, s); break;
-        case 4: sym2_launch<128, 8, 1>(a, s); break;   // one-wave K=16 measured 30 % slower
-        case 5: sym2_launch<256, 8, 1>(a, s); break;
-        case 6: sym2_launch<512, 8, 1>(a, s); break;
-        default: sym2_launch<1024, 8, 1>(a, s); break;
+        case 4: sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(a, s); break;   // one-wave K=16 measured 30 % slower
+        case 5: sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+        case 6: sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+        default: sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(a, s); break;
     }
 }
 

@@ -150,6 +150,10 @@ __device__ __forceinline__ Sym2Row sym2_detail(const Sym2Args &a, const RowRef &
     return r;
 }
 
+#ifndef SYM2_DB_MAX
+#define SYM2_DB_MAX 8   // K up to which a team double-buffers the next row's columns in registers
+#endif
+
 // range reduction of a 32-bit hash onto [0, n)
 __device__ __forceinline__ uint32_t reduce32(uint32_t h, uint32_t n) {
     return (uint32_t)(((uint64_t)h * n) >> 32);
@@ -165,7 +169,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     using TM = Team<TEAM>;
     constexpr int LPASS = K > 4 ? K / 4 : 1;   // list capacity <= U/4 <= LPASS * TEAM
     constexpr int CH = K < 8 ? K : 8;          // items per register chunk
-    constexpr bool DB = K <= 8;                // next row's columns gathered during this row's work
+    constexpr bool DB = K <= SYM2_DB_MAX;      // next row's columns gathered during this row's work
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Sym2Layout L = a.lay;
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
@@ -284,7 +288,9 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             for (int t = 0; t < CH; ++t) {
                 const bool cand = (old[t] & bitm[t]) != 0u;
                 candm |= (cand ? 1u : 0u) << (k0 + t);
-                atomicOr(&f2[word[t]], cand ? bitm[t] : 0u);
+                // candidates only (a few %): an all-lane atomic at random words
+                // doubled the LDS bank conflicts of the pass
+                if (cand) atomicOr(&f2[word[t]], bitm[t]);
             }
         }
         TM::sync();
@@ -483,6 +489,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             for (int k = 0; k < K; ++k) c[k] = cn[(DB ? k : 0)];
         } else if (nrow >= 0) {
             gather(nP, c);   // one register set: other waves cover the load latency
+            TM::sync();      // every wave has read the staging arrays before the next stage()
         }
         row = nrow;
         P = nP;
