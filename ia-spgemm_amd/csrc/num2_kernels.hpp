@@ -1,0 +1,254 @@
+// num2_kernels.hpp — numeric pass of the streaming rows (rows whose
+// duplicates fit their list, dupn >= 0) with C written through LDS in whole,
+// ascending, 16-byte-aligned pieces.
+//
+// Restates CSR_MUL_CSR's second loop (IA-SPGEMM-CPU_release/detail/csr/
+// common_csr.h:133-189) for rows the symbolic pass has already resolved: bit p
+// of a row's first-touch bitmap says whether product p is its column's first
+// touch, its rank (set bits before it) is the column's discovery index, and
+// the entry lands at row_start + nnz-1-rank (reverse first-touch, the
+// reference's linked-list order) or row_start + rank (COO_MUL_COO's order);
+// the value is 0.0 + a*b (or a*b for COO).  A duplicate's product is parked at
+// dupval[dup_off + p - rank] for the fix-up kernels, which add it to its
+// column's entry in product order.
+//
+// Unit of work: one wave takes 64 consecutive A entries of one row (a unit);
+// their products are one contiguous product range of the row, so the C
+// entries they produce are one contiguous range of C.  Lanes walk the range
+// in 64-aligned windows of the row's product space (bitmap words and their
+// prefix counts are then two scalar loads per window), the window's entries
+// from per-window start masks (the flat pass's mapping), and the first
+// touches are staged in LDS by rank, PASS of them at a time, then leave as
+// ascending 16-byte stores (4 columns / 2 values per lane) — measured: the
+// flat pass's reverse-order 4- and 8-byte scatter stores took ~3 of its 5 ms.
+#pragma once
+
+#include "spgemm_kernels.hpp"
+
+namespace ias {
+namespace dev {
+
+constexpr int N2_ENT = 64;     // A entries per unit (one per lane)
+constexpr int N2_WPB = 4;      // waves (units) per workgroup
+
+struct Num2Unit {
+    int32_t row;
+    int32_t e0;   // first A entry of the unit within the row
+};
+
+struct Num2Args {
+    Rows A;                  // A's rows (entry ranges)
+    AxView ax;               // expanded A: B-row start / length, A value per entry
+    const int64_t *axp;      // product offset of every A entry
+    const int64_t *poff;     // product offset of every row
+    const int32_t *bcol;
+    const double *bval;
+    const Num2Unit *units;
+    int64_t nunits;
+    Bitmap bm;
+    const int64_t *dup_off;
+    double *dupval;
+};
+
+// Units: every streaming row with products gets ceil(entries / 64) of them.
+__global__ void k_num2_count(Rows A, int64_t rows, const int32_t *dupn, const int32_t *prod, int32_t *cnt) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    int64_t s;
+    int32_t n;
+    A.row(r, s, n);
+    cnt[r] = (dupn[r] >= 0 && prod[r] > 0) ? (n + N2_ENT - 1) / N2_ENT : 0;
+}
+__global__ void k_num2_fill(int64_t rows, const int32_t *cnt, const int64_t *uoff, Num2Unit *units) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int32_t c = cnt[r];
+    const int64_t o = uoff[r];
+    for (int32_t i = 0; i < c; ++i) units[o + i] = Num2Unit{(int32_t)r, i * N2_ENT};
+}
+
+// 16-byte non-temporal store (C is not read back by this pass)
+typedef uint32_t n2_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16(void *p, uint4 v) {
+    const n2_u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, (n2_u32x4 *)p);
+}
+
+// N2_K windows per step: their gathers are in flight together, and the next
+// step's gathers are issued before this step's stores (vmcnt retires loads and
+// stores in issue order, so a load behind a store would wait for the store).
+#ifndef N2_K
+#define N2_K 4
+#endif
+
+__global__ __launch_bounds__(64 * N2_WPB) void k_num2(Num2Args a, Out out) {
+    constexpr int K = N2_K;
+    constexpr int PASS = 64 * K;   // staged C entries per step (at most one per product)
+    struct Ent {
+        int64_t bs;   // B-row start - row-relative first product of the entry
+        double av;
+    };
+    __shared__ Ent ent[N2_WPB][N2_ENT];
+    __shared__ unsigned long long wmask[N2_WPB][K];
+    __shared__ __attribute__((aligned(16))) int32_t scol[N2_WPB][PASS];
+    __shared__ __attribute__((aligned(16))) double sval[N2_WPB][PASS];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int64_t u = (int64_t)blockIdx.x * N2_WPB + w;
+    if (u >= a.nunits) return;
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    const Num2Unit un = a.units[u];
+    const int64_t row = un.row;
+    int64_t as;
+    int32_t an;
+    a.A.row(row, as, an);
+    const int64_t q0 = as - a.A.base() + un.e0;
+    const int32_t n = min(N2_ENT, an - un.e0);
+    const int64_t prow = a.poff[row];
+    // this lane's entry
+    int32_t bl = 0, rel = 0;
+    int64_t bs = 0;
+    double av = 0.0;
+    if (lane < n) {
+        bl = a.ax.blen[q0 + lane];
+        bs = a.ax.bstart[q0 + lane];
+        av = a.ax.aval[q0 + lane];
+        rel = (int32_t)(a.axp[q0 + lane] - prow);
+    }
+    // the unit's products [pa, pb) of the row
+    const int32_t pa = __builtin_amdgcn_readfirstlane(rel);
+    const int32_t pb = __builtin_amdgcn_readlane(rel + bl, n - 1);
+    if (pb <= pa) return;
+    // non-empty entries, compacted in order
+    const uint64_t ne = __ballot(bl > 0);
+    if (bl > 0) ent[w][__popcll(ne & ((1ull << lane) - 1ull))] = Ent{bs - rel, av};
+    const int64_t cst = out.start(row);
+    const int32_t nnz = out.len[row];
+    const int64_t bmo = a.bm.off[row];
+    const int64_t dbase = a.dup_off[row];
+    const int64_t cbase = out.order == 0 ? cst + nnz - 1 : cst;   // C position of rank 0
+    const uint64_t upto = (2ull << lane) - 1ull;                // bits 0..lane
+    const uint32_t below = (1u << (lane & 31)) - 1u;
+    // 16-byte pieces start where the destination address is 16-byte aligned
+    const int64_t cph = (int64_t)(((uintptr_t)out.col >> 2) & 3u);
+    const int64_t vph = (int64_t)(((uintptr_t)out.val >> 3) & 1u);
+    // rank of the unit's first product = the row's first touches before pa
+    int32_t r0;
+    {
+        const uint32_t wd = a.bm.bits[bmo + (pa >> 5)];
+        r0 = (int32_t)a.bm.pref[bmo + (pa >> 5)] + __popc(wd & ((1u << (pa & 31)) - 1u));
+    }
+    struct Step {
+        int32_t c[K];
+        double bv[K];
+        int32_t e[K];
+        uint32_t word[K], pre[K];   // the lane's bitmap word and its prefix count
+    };
+    // gathers of the step at window pw0.  Branch-free (clamped addresses for
+    // the lanes and words outside the unit), so that the wait for a step's
+    // loads counts exactly the loads issued after them.
+    const int64_t lastw = bmo + ((pb - 1) >> 5);
+    auto load = [&](int32_t pw0, Step &S) {
+        if (lane < K) wmask[w][lane] = 0ull;
+        wave_sync();
+        if (bl > 0 && rel >= pw0 && rel < pw0 + PASS)
+            atomicOr(&wmask[w][(rel - pw0) >> 6], 1ull << ((rel - pw0) & 63));
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t pw = pw0 + 64 * k;
+            const int32_t p = pw + lane;
+            const int ecur = __popcll(__ballot(bl > 0 && rel < pw));
+            S.e[k] = max(ecur + __popcll(wmask[w][k] & upto) - 1, 0);
+            const int64_t kb = (p >= pa && p < pb) ? ent[w][S.e[k]].bs + p : 0;
+            S.c[k] = a.bcol[kb];
+            S.bv[k] = a.bval[kb];
+            const int64_t wi = min(bmo + (pw >> 5) + (lane >> 5), lastw);
+            S.word[k] = a.bm.bits[wi];
+            S.pre[k] = a.bm.pref[wi];
+        }
+    };
+    // stage the step's first touches by rank, park its duplicates, flush
+    auto store = [&](int32_t pw0, const Step &S) {
+        int nft = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int32_t p = pw0 + 64 * k + lane;
+            const uint32_t word = S.word[k], pre = S.pre[k];
+            const bool in = p >= pa && p < pb;
+            const bool ft = in && ((word >> (lane & 31)) & 1u);
+            const int32_t rk = (int32_t)(pre + (uint32_t)__popc(word & below));
+            const double prod = ent[w][S.e[k]].av * S.bv[k];
+            if (ft) {
+                scol[w][rk - r0] = S.c[k];
+                sval[w][rk - r0] = out.first_assign ? prod : 0.0 + prod;
+            } else if (in) {
+                a.dupval[dbase + (p - rk)] = prod;
+            }
+            nft += __popcll(__ballot(ft));
+        }
+        wave_sync();
+        // C positions of the staged ranks r0 .. r0 + nft - 1: [xlo, xhi)
+        const int64_t xlo = out.order == 0 ? cbase - (r0 + nft - 1) : cbase + r0;
+        const int64_t xhi = xlo + nft;
+        const int64_t i0 = out.order == 0 ? cbase - r0 : -(cbase + r0);
+        auto idx = [&](int64_t x) -> int32_t { return out.order == 0 ? (int32_t)(i0 - x) : (int32_t)(x + i0); };
+        // whole 16-byte pieces: [a4, e4) of the columns, [a2, e2) of the values
+        const int64_t a4 = ((xlo + cph + 3) & ~3ll) - cph, e4 = ((xhi + cph) & ~3ll) - cph;
+        const int64_t a2 = ((xlo + vph + 1) & ~1ll) - vph, e2 = ((xhi + vph) & ~1ll) - vph;
+#pragma unroll
+        for (int it = 0; it < (PASS / 4 + WAVE) / WAVE; ++it) {
+            const int64_t x = a4 + 4ll * (lane + WAVE * it);
+            if (x + 4 <= e4) {
+                uint4 v;
+                v.x = (uint32_t)scol[w][idx(x)];
+                v.y = (uint32_t)scol[w][idx(x + 1)];
+                v.z = (uint32_t)scol[w][idx(x + 2)];
+                v.w = (uint32_t)scol[w][idx(x + 3)];
+                st16(&out.col[x], v);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < (PASS / 2 + WAVE) / WAVE; ++it) {
+            const int64_t x = a2 + 2ll * (lane + WAVE * it);
+            if (x + 2 <= e2) {
+                const double d0 = sval[w][idx(x)], d1 = sval[w][idx(x + 1)];
+                uint4 v;
+                __builtin_memcpy(&v.x, &d0, 8);
+                __builtin_memcpy(&v.z, &d1, 8);
+                st16(&out.val[x], v);
+            }
+        }
+        // the partial pieces at both ends: lanes 0-2 / 3-5 columns, 6 / 7 values
+        int64_t xc = -1, xv = -1;
+        if (lane < 3) xc = xlo + lane < min(a4, xhi) ? xlo + lane : -1;
+        else if (lane < 6) xc = max(e4, a4) + (lane - 3) < xhi ? max(e4, a4) + (lane - 3) : -1;
+        else if (lane == 6) xv = xlo < min(a2, xhi) ? xlo : -1;
+        else if (lane == 7) xv = max(e2, a2) < xhi ? max(e2, a2) : -1;
+        if (xc >= 0) __builtin_nontemporal_store(scol[w][idx(xc)], &out.col[xc]);
+        if (xv >= 0) __builtin_nontemporal_store(sval[w][idx(xv)], &out.val[xv]);
+        r0 += nft;
+        wave_sync();
+    };
+    // two step buffers, alternating (no register copies between steps)
+    Step s0, s1;
+    int32_t pw0 = (pa >> 6) << 6;
+    load(pw0, s0);
+    for (;;) {
+        load(pw0 + PASS, s1);   // past the unit: clamped, harmless
+        store(pw0, s0);
+        pw0 += PASS;
+        if (pw0 >= pb) break;
+        load(pw0 + PASS, s0);
+        store(pw0, s1);
+        pw0 += PASS;
+        if (pw0 >= pb) break;
+    }
+}
+
+}  // namespace dev
+}  // namespace ias

@@ -6,6 +6,7 @@
 #include "spgemm_kernels.hpp"
 #include "onepass_kernels.hpp"
 #include "sym2_kernels.hpp"
+#include "num2_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
 
@@ -28,9 +29,12 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
 }
 
 // stv: the row's streaming state (-2: none given; >= 0: a streaming row with
-// stv duplicates -> the fix-up bin when it has any, nothing to do otherwise).
+// stv duplicates -> the fix-up bin when it has any, nothing to do otherwise;
+// -3: a table-path row without a first-touch bitmap too long for the LDS
+// bins -> the per-row global table).
 __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv, int32_t ent2 = 0) {
     if (k <= 0) return 0;
+    if (stv == -3) return sp.nval + 2;
     if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), longer (sorted)
         if (stv == 0) return 0;
         return sp.nval + 3 + sp.ndw + (stv > 256 ? 2 : (stv > 16 ? 1 : 0));
@@ -1105,9 +1109,13 @@ __global__ void k_fill_rows(const int64_t *ptr, int64_t rows, int32_t *row_idx) 
 }
 
 // ---------------------------------------------------------------- row sort
-// IAS_ORDER_SORTED: bitonic sort of (col, val) per row, in LDS up to 8192
-// entries, in a per-row global workspace beyond.  Columns of a row are
-// distinct, so the order is unique.
+// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (2048 by default,
+// IAS_SORT_WIDE_MIN moves it, up to 8192) get a bitonic sort of (col, val) in
+// LDS; the LDS bins above 2048 entries (4096 / 8192) only run when the knob is
+// raised.  Longer rows go through one segmented radix sort over a compact
+// workspace (k_wide_gather), or, when that workspace cannot be had (or
+// IAS_SORT_GLOBAL=1), a bitonic sort per row in a global workspace
+// (k_sort_global).  Columns of a row are distinct, so the order is unique.
 template <int TEAM>
 __device__ __forceinline__ void bitonic(int32_t *sk, double *sv, uint32_t cap) {
     const int lane = Team<TEAM>::lane();
@@ -1256,6 +1264,17 @@ __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const in
     }
 }
 
+// entries of every listed wide row (the compact radix workspace is their scan)
+__global__ void k_wide_len(const RowRef *list, int32_t count, const int64_t *ptr, const int32_t *len,
+                           int64_t stride, int32_t *wl) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    int64_t o;
+    int32_t n;
+    sort_row_span(ptr, len, stride, list[i].row, o, n);
+    wl[i] = n;
+}
+
 __global__ void k_row_len(const int64_t *ptr, int64_t rows, int32_t *len) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < rows) len[i] = (int32_t)(ptr[i + 1] - ptr[i]);
@@ -1314,10 +1333,19 @@ constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 // lane, 4 teams per workgroup: no workgroup barrier per row), 4..7 = 128- to
 // 1024-lane teams with K = 8 (one-wave teams with K = 16 / 32 measured slower:
 // 160-256 VGPRs, 2-3 waves per SIMD).
-constexpr int32_t SYM2_MAX = 8192;
+#ifndef SYM2_WIDE
+#define SYM2_WIDE 1   // rows of 8193..16384 products on sym2 (else the partitioned path)
+#endif
+constexpr int32_t SYM2_MAX = SYM2_WIDE ? 16384 : 8192;
 constexpr int SYM2_WAVE_CFG_MAX = 3;
-static constexpr BinCfg SYM2_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {768, 4},  {1024, 4},
-                                       {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6}, {6144, 7}, {SYM2_MAX, 7}};
+constexpr int SYM2_CFG_WIDE = 8;   // 16 products per lane of a 1024-lane team, one-wave (compact) layout
+static constexpr BinCfg SYM2_BINS[] = {{64, 0},    {128, 1},  {256, 2},  {512, 3},  {768, 4},
+                                       {1024, 4},  {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6},
+                                       {6144, 7},  {8192, 7},
+#if SYM2_WIDE
+                                       {12288, SYM2_CFG_WIDE}, {SYM2_MAX, SYM2_CFG_WIDE}
+#endif
+};
 constexpr int N_SYM2 = sizeof(SYM2_BINS) / sizeof(SYM2_BINS[0]);
 static bool sym2_on() {
     static const bool on = [] {
@@ -1326,6 +1354,16 @@ static bool sym2_on() {
     }();
     return on;
 }
+// IAS_NUM2=0: the streaming rows take the flat numeric pass (k_numeric_flat)
+// instead of the row-unit pass with LDS-staged C writes (k_num2).
+static bool num2_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_NUM2");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
 static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
@@ -1350,7 +1388,7 @@ static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upp
 // duplicate-list capacity of a symbolic bin: rows with more duplicate
 // products than this take the table path in the numeric pass
 static constexpr int32_t dcap_for(int32_t upper) {
-    return upper / 8 < 8 ? 8 : (upper / 8 > 1024 ? 1024 : upper / 8);
+    return upper / 8 < 8 ? 8 : (upper / 8 > 2048 ? 2048 : upper / 8);
 }
 constexpr int32_t PART_DCAP_DIV = 8;   // partitioned rows: list of min(products / 8, FIXBIG_CAP)
 
@@ -1522,7 +1560,10 @@ static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, u
 }
 
 static Sym2Layout sym2_layout(int32_t upper, int cfg) {
-    return Sym2Layout::for_bound((uint32_t)upper, cfg <= SYM2_WAVE_CFG_MAX);
+    // 8 filter bits keep the widest bin's team within one CU's LDS
+    return Sym2Layout::for_bound((uint32_t)upper, cfg == SYM2_CFG_WIDE     ? Sym2Layout::WIDE
+                                                  : cfg <= SYM2_WAVE_CFG_MAX ? Sym2Layout::ONE_WAVE
+                                                                             : Sym2Layout::TEAM_LAYOUT);
 }
 
 template <int TEAM, int K, int TPW, int WPE = 1>
@@ -1548,7 +1589,8 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
         case 4: sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(a, s); break;   // one-wave K=16 measured 30 % slower
         case 5: sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(a, s); break;
         case 6: sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(a, s); break;
-        default: sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+        case 7: sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+        default: sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(a, s); break;   // SYM2_CFG_WIDE
     }
 }
 
@@ -1876,7 +1918,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 return e ? atoi(e) : 0;
             }();
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
-                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl};
+                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl, DW_MAX};
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);
         }
@@ -1894,6 +1936,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // ---- row pointer of C, numeric binning by nnz (and products / nnz)
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
     IAS_TRY(reserve(B_NITEM, sizeof(PartItem) * (size_t)(rows + flops / NUM_PART_CAP + 2)));
+    n2_units = 0;
     if (rows > 0) {
         k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
                                                           &dc2->max_nnz);
@@ -1907,6 +1950,19 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
             nullptr, dc2, nullptr, nullptr, 0);
     CHECK_LAUNCH("numeric binning", s);
+        if (num2_on()) {
+            // work units of the row-unit numeric pass: 64 A entries of a streaming row
+            IAS_TRY(reserve(B_N2CNT, sizeof(int32_t) * (size_t)rows));
+            IAS_TRY(reserve(B_N2OFF, sizeof(int64_t) * (size_t)(rows + 1)));
+            IAS_TRY(reserve(B_N2UNIT, sizeof(Num2Unit) * (size_t)(rows + a_entries / N2_ENT + 1)));
+            int32_t *cnt = as<int32_t>(bufs[B_N2CNT]);
+            int64_t *uoff = as<int64_t>(bufs[B_N2OFF]);
+            k_num2_count<<<grid_for(rows, 256), 256, 0, s>>>(A, rows, sa.dupn, as<int32_t>(bufs[B_PROD]), cnt);
+            scan_i32(cnt, rows, as<int64_t>(bufs[B_PART]), uoff, s);
+            k_num2_fill<<<grid_for(rows, 256), 256, 0, s>>>(rows, cnt, uoff, as<Num2Unit>(bufs[B_N2UNIT]));
+            CHECK_LAUNCH("k_num2_fill", s);
+            HIPC(hipMemcpyAsync(&n2_units, uoff + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        }
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
     }
@@ -1941,7 +1997,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
 }
 
 ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ias_report *rep) {
-    (void)A;
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     const int64_t rows = n_rows;
@@ -1993,7 +2048,15 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
         const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 2048);
         HIPC(hipEventRecord(ev[5], t));
-        k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
+        if (num2_on()) {
+            if (n2_units > 0) {
+                const Num2Args na{A, ax, fa.axp, fa.poff, B.col, B.val, as<Num2Unit>(bufs[B_N2UNIT]), n2_units,
+                                  bm, sa.dup_off, fa.dupval};
+                k_num2<<<(unsigned)((n2_units + N2_WPB - 1) / N2_WPB), 64 * N2_WPB, 0, t>>>(na, out);
+            }
+        } else {
+            k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
+        }
         HIPC(hipEventRecord(ev[6], t));
         CHECK_LAUNCH("k_numeric_flat", t);
         const int fb = ns.nval + 3 + N_DW;
@@ -2267,21 +2330,40 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     HIPC(hipStreamSynchronize(s));
     const int wide = spec.nval + 2;
     const int32_t nwide = hc.count[wide];
-    const bool radix = nwide > 0 && hc.ws_slots < (unsigned long long)INT32_MAX;
-    size_t rtmp = 0;
-    const size_t slots = (size_t)hc.ws_slots;
-    if (radix) {
-        HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(
-            nullptr, rtmp, (const int32_t *)nullptr, (int32_t *)nullptr, (const double *)nullptr,
-            (double *)nullptr, (int)slots, nwide, (const int64_t *)nullptr, (const int64_t *)nullptr,
-            0, 31, s));
-        IAS_TRY(plan->reserve(ias_plan::B_TMP4, 24ull * slots + 16ull * nwide + rtmp + 256));
-    } else if (nwide > 0) {
-        IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
-    }
     int64_t st[MAX_BINS];
     bin_starts(hc, st);
     auto lst = [&](int b) { return lists + st[b]; };
+    // wide rows: compact radix workspace (their entries, scanned), else the
+    // padded per-row bitonic workspace (12 B per binning slot)
+    static const bool force_global = [] {
+        const char *e = getenv("IAS_SORT_GLOBAL");
+        return e && *e == '1';
+    }();
+    bool radix = false;
+    size_t rtmp = 0, slots = 0;
+    int64_t *coff = nullptr;
+    if (nwide > 0 && !force_global) {
+        const int64_t nb = (nwide + SCAN_TILE - 1) / SCAN_TILE;
+        IAS_TRY(plan->reserve(ias_plan::B_TMP5, 4ull * nwide + 8ull * (nwide + 1) + 8ull * (nb + 2) + 64));
+        int32_t *wl = (int32_t *)plan->bufs[ias_plan::B_TMP5].p;
+        coff = (int64_t *)(((uintptr_t)(wl + nwide) + 7) & ~(uintptr_t)7);
+        int64_t *part = coff + nwide + 1;
+        k_wide_len<<<grid_for(nwide, 256), 256, 0, s>>>(lst(wide), nwide, ptr, len, stride, wl);
+        scan_i32(wl, nwide, part, coff, s);
+        int64_t total = 0;
+        HIPC(hipMemcpyAsync(&total, coff + nwide, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+        slots = (size_t)total;
+        if (total < (int64_t)INT32_MAX) {
+            HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(
+                nullptr, rtmp, (const int32_t *)nullptr, (int32_t *)nullptr, (const double *)nullptr,
+                (double *)nullptr, (int)slots, nwide, (const int64_t *)nullptr, (const int64_t *)nullptr,
+                0, 31, s));
+            radix = plan->reserve(ias_plan::B_TMP4, 24ull * slots + 16ull * nwide + rtmp + 256) == IAS_SUCCESS;
+            if (!radix) (void)hipGetLastError();   // allocation failure: take the bitonic workspace
+        }
+    }
+    if (nwide > 0 && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     int c;
     if ((c = hc.count[1]) > 0)
         k_sort_lds<32, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
@@ -2305,13 +2387,13 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
         int32_t *kout = kin + slots;
         void *tmp = (void *)(((uintptr_t)(kout + slots) + 255) & ~(uintptr_t)255);
         const dim3 g(c, 16);
-        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val, kin, vin, beg,
+        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, coff, ptr, len, stride, col, val, kin, vin, beg,
                                         end, false);
         HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, rtmp, (const int32_t *)kin, kout,
                                                          (const double *)vin, vout, (int)slots, c,
                                                          (const int64_t *)beg, (const int64_t *)end,
                                                          0, 31, s));
-        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val, kout, vout,
+        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, coff, ptr, len, stride, col, val, kout, vout,
                                         beg, end, true);
     } else if (c > 0) {
         k_sort_global<<<c, 1024, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val,

@@ -55,12 +55,14 @@ struct ias_plan {
     enum {
         B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
-        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4,
+        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5,
         // single-pass path (onepass)
         B_OPCF, B_OPBF, B_OPCID, B_OPBPOS, B_OPCROW, B_OPSTAT, B_OPMISC, B_OPBROW, B_OPBLEN, B_OPBPTR,
         B_OPBCOL, B_OPBVAL, B_OPBCPTR,
         // partition buckets of the symbolic pass
-        B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN, B_COUNT
+        B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
+        // work units of the row-unit numeric pass (num2)
+        B_N2CNT, B_N2OFF, B_N2UNIT, B_COUNT
     };
     struct Buf {
         void *p = nullptr;
@@ -94,6 +96,7 @@ struct ias_plan {
     int32_t num_count[ias::MAX_BINS] = {};
     unsigned long long num_items = 0;
     int64_t st_prod = 0, st_nnz = 0;
+    int64_t n2_units = 0;   // work units of the row-unit numeric pass
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;

@@ -68,12 +68,14 @@ struct Sym2Layout {
     __host__ __device__ uint32_t heavy_slots() const { return (uint32_t)((ebase() - f1()) / 4); }
     // one-wave teams (wide rows on one wave: LDS per wave is the limit) keep
     // 8 filter bits and an eighth of the products for the exact list; the
-    // workgroup teams 16 bits and a quarter
-    __host__ static Sym2Layout for_bound(uint32_t upper, bool one_wave) {
+    // workgroup teams 16 bits and a quarter; the widest bin (16384 products,
+    // one team per CU) 8 bits and a quarter
+    enum Mode { TEAM_LAYOUT = 0, ONE_WAVE = 1, WIDE = 2 };
+    __host__ static Sym2Layout for_bound(uint32_t upper, Mode m) {
         Sym2Layout L;
         L.U = upper;
-        L.FW = one_wave ? upper / 4 : upper / 2;
-        L.LC = one_wave ? upper / 8 : upper / 4;
+        L.FW = m == TEAM_LAYOUT ? upper / 2 : upper / 4;
+        L.LC = m == ONE_WAVE ? upper / 8 : upper / 4;
         L.ES = 2 * L.LC;
         L.EC = upper / 8;
         L.W = (upper + 63) / 64;
@@ -95,6 +97,8 @@ struct Sym2Args {
     int32_t *gdupt;
     int32_t dcap;              // duplicate targets allocated per row (dup_off spacing): more -> table path
     int32_t ablate;            // timing experiments only (IAS_S2_ABLATE): 2 no gathers
+    int32_t bm_need;           // heavy rows above this nnz get dupn -3: the numeric pass's
+                               // partitioned path needs a bitmap they do not have
 };
 
 // What a team prefetches of a row before it works on it.
@@ -165,10 +169,10 @@ __device__ __forceinline__ uint32_t fib(int32_t c) { return (uint32_t)c * 0x9E37
 template <int TEAM, int K, int TPW, int WPE>
 __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sym2(Sym2Args a) {
     static_assert(TEAM >= WAVE && (TEAM <= WAVE || TPW == 1), "teams are whole waves; multi-wave teams own the WG");
-    static_assert(TEAM == WAVE ? K <= 32 : K <= 8, "finish() covers the bitmap words in one pass");
+    static_assert(TEAM == WAVE ? K <= 32 : K <= 16, "finish() covers the bitmap words in one pass");
     using TM = Team<TEAM>;
     constexpr int LPASS = K > 4 ? K / 4 : 1;   // list capacity <= U/4 <= LPASS * TEAM
-    constexpr int CH = K < 8 ? K : 8;          // items per register chunk
+    constexpr int CH = K < 8 ? K : (TEAM > WAVE && K > 8 ? 4 : 8);   // items per register chunk (1024-lane teams: 128 VGPRs)
     constexpr bool DB = K <= SYM2_DB_MAX;      // next row's columns gathered during this row's work
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Sym2Layout L = a.lay;
@@ -433,7 +437,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         }
         if (lane == 0) {
             a.nnz_row[row] = nnz;
-            a.dupn[row] = heavy ? -1 : P - nnz;
+            a.dupn[row] = heavy ? (nnz > a.bm_need ? -3 : -1) : P - nnz;
             *lcount = 0;   // every lane read it before this pass's barriers
         }
         clear_tables();   // the caller's barrier follows
