@@ -11,14 +11,18 @@ preallocated device arrays.  `--engine onepass` times the single-pass chunk
 engine instead (ias_csr_mul_csr_into with IAS_ONEPASS=1; C's capacity =
 flops(A*A) >= nnz(C), reported by a capacity-0 call before timing).
 
-Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15,
-edge factor 20, scale 20 + log2(N) — at N=1 this is the north-star headline
-matrix (1M rows, ~20 nnz/row; SURVEY.md §8 K3'), at N=8 a 8M-row matrix of the
-K4 family.  Rows are sharded by equal products (flops prefix) across ranks with
-B replicated (broadcast once over RCCL before timing); per-rank work is fixed
-as N grows, hence "scaling": "weak".  No collective inside the timed region
-(C stays sharded; the allgatherv of C is measured separately by
-tools/gather_bench.py).
+Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15.
+N=1: the north-star headline matrix K3' (2^20 rows, edge factor 20, seed 2;
+SURVEY.md §8).  N>1: the K4 family, 2^(20+log2 N) rows, edge factor 24,
+seed 3 — N=8 is BASELINE's K4 (8M x 8M, avg 24 nnz/row).  Rows are sharded by
+estimated device cost (ias_partition_rows) across ranks with B replicated
+(broadcast once over RCCL before timing); per-rank work grows with the
+matrix, hence "scaling": "weak".  No collective inside the timed region (C
+stays sharded).  For N>1 the exchange step is measured after the timed loop
+(`allgatherv` in the line): one step compute-only and one step
+compute + the RCCL allgatherv that concatenates C on every rank
+(ias/dist.py gather_csr), max over ranks; `--no-gather` skips it,
+tools/gather_bench.py runs it alone with more repetitions.
 """
 import argparse
 import ctypes as C
@@ -47,7 +51,7 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
@@ -60,17 +64,23 @@ def parse():
     p.add_argument("--engine", default="twophase", choices=["onepass", "twophase"])
     p.add_argument("--no-host-e2e", action="store_true",
                    help="skip the one PCIe-inclusive call with host operands (N=1 only)")
-    p.add_argument("--as-rank", type=int, default=None,
+    p.add_argument("--as-rank", default=None,
                    help="single process: run only rank R's shard of the --gpus N workload "
-                        "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers)")
-    return p.parse_args()
+                        "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers); "
+                        "'R1,R2,...' or 'all' run several shards one after the other, one line each")
+    p.add_argument("--no-gather", action="store_true", help="N>1: skip the allgatherv measurement")
+    p.add_argument("--gather-reps", type=int, default=1, help="N>1: repetitions of the allgatherv measurement")
+    return p.parse_args(argv)
 
 
 def workload(cfg: str, world: int):
     if cfg == "auto":
-        scale = 20 + int(round(math.log2(max(world, 1))))
-        return "rmat", dict(scale=scale, ef=20, seed=2), (
-            f"R-MAT 2^{scale}, edge factor 20, (a,b,c)=(.45,.15,.15); N=1: north-star K3'")
+        if world <= 1:
+            return "rmat", dict(scale=20, ef=20, seed=2), (
+                "R-MAT 2^20, edge factor 20, seed 2, (a,b,c)=(.45,.15,.15): north-star K3'")
+        scale = 20 + int(round(math.log2(world)))
+        return "rmat", dict(scale=scale, ef=24, seed=3), (
+            f"R-MAT 2^{scale}, edge factor 24, seed 3, (a,b,c)=(.45,.15,.15): K4 family (N=8: BASELINE K4)")
     kind, prm, desc = CONFIGS[cfg]
     return kind, dict(prm), desc
 
@@ -86,8 +96,20 @@ def generate(kind, prm):
     raise ValueError(kind)
 
 
-def main():
-    args = parse()
+def as_rank_list(spec, n):
+    if spec is None:
+        return None
+    if spec == "all":
+        return list(range(n))
+    rs = [int(x) for x in str(spec).split(",") if x != ""]
+    for r in rs:
+        if not 0 <= r < n:
+            raise SystemExit(f"--as-rank {r} outside 0..{n - 1}")
+    return rs
+
+
+def main(argv=None):
+    args = parse(argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -105,21 +127,20 @@ def main():
         dist.init_process_group(backend="nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    as_ranks = as_rank_list(args.as_rank, world_req) if not dist_on else None
 
     kind, prm, desc = workload(args.config, world_req)
     # ---------------- inputs: rank 0 generates, B replicated by broadcast
     t_gen = time.time()
     meta = torch.zeros(4, dtype=torch.int64)
+    nparts = world_req if (as_ranks is not None) else world
     if rank == 0:
         A = generate(kind, prm)
         meta[:] = torch.tensor([A.rows, A.cols, A.nnz, ias.flops(A, A)])
-        nparts = world_req if (args.as_rank is not None and not dist_on) else world
         bounds = (C.c_int64 * (nparts + 1))()
         sa = A.struct()
         ias.check(ias.lib.ias_partition_rows(C.byref(sa), C.byref(sa), nparts, bounds), "partition")
         bnd = torch.tensor(list(bounds), dtype=torch.int64)
-        if nparts != world:   # --as-rank: this process is rank R of nparts
-            bnd = bnd[args.as_rank:args.as_rank + 2].clone()
     else:
         A = None
         bnd = torch.zeros(world + 1, dtype=torch.int64)
@@ -149,210 +170,279 @@ def main():
                        C.cast(C.c_void_p(ci.data_ptr()), ias.i32p),
                        C.cast(C.c_void_p(va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
 
-    r0, r1 = int(bnd[rank]), int(bnd[rank + 1])
-    rp_host = rp[r0:r1 + 1].cpu()
     Bm = dcsr(0, rows, rp, nnz_a)
-    Am = dcsr(r0, r1, rp, int(rp_host[-1] - rp_host[0]))
     plan = C.c_void_p()
     ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
     order = ias.ORDER_SORTED if args.order == "sorted" else ias.ORDER_REFERENCE
-
     if args.engine == "onepass":
         os.environ["IAS_ONEPASS"] = "1"
-    if args.engine == "twophase":
-        nnz_c = C.c_int64(0)
-        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None, None), "nnz")
-        cap = int(nnz_c.value)
-    else:
-        # capacity = flops of this shard (an upper bound of nnz(C) known from A and B alone):
-        # a capacity-0 call reports it without writing C
-        probe = ias.Report()
-        c_rp0 = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
-        C0 = ias.Csr(r1 - r0, cols, 0, C.cast(C.c_void_p(c_rp0.data_ptr()), ias.i64p), None, None,
-                     ias.MEMORY_DEVICE, local)
-        st = ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(C0), 0, C.byref(probe))
-        if st not in (0, 11):
-            ias.check(st, "into (capacity probe)")
-        cap = int(probe.flops)
-        del c_rp0
-    c_rp = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
-    c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
-    c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
-    Cm = ias.Csr(r1 - r0, cols, cap, C.cast(C.c_void_p(c_rp.data_ptr()), ias.i64p),
-                 C.cast(C.c_void_p(c_ci.data_ptr()), ias.i32p),
-                 C.cast(C.c_void_p(c_va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
-    rep = ias.Report()
-    rep_s = ias.Report()
 
-    def step_onepass():
-        Cm.nnz = cap
-        ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
-                                               C.byref(rep)), "into")
-        return rep
+    def run_shard(shard):
+        """Warm-up + the timed loop over this process's shard `shard` of A;
+        returns the JSON line (rank 0's view) and the shard's C tensors."""
+        r0, r1 = int(bnd[shard]), int(bnd[shard + 1])
+        rp_host = rp[r0:r1 + 1].cpu()
+        Am = dcsr(r0, r1, rp, int(rp_host[-1] - rp_host[0]))
+        if args.engine == "twophase":
+            nnz_c = C.c_int64(0)
+            ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None, None),
+                      "nnz")
+            cap = int(nnz_c.value)
+        else:
+            # capacity = flops of this shard (an upper bound of nnz(C) known from A and B alone):
+            # a capacity-0 call reports it without writing C
+            probe = ias.Report()
+            c_rp0 = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
+            C0 = ias.Csr(r1 - r0, cols, 0, C.cast(C.c_void_p(c_rp0.data_ptr()), ias.i64p), None, None,
+                         ias.MEMORY_DEVICE, local)
+            st = ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(C0), 0, C.byref(probe))
+            if st not in (0, 11):
+                ias.check(st, "into (capacity probe)")
+            cap = int(probe.flops)
+            del c_rp0
+        c_rp = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
+        c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
+        Cm = ias.Csr(r1 - r0, cols, cap, C.cast(C.c_void_p(c_rp.data_ptr()), ias.i64p),
+                     C.cast(C.c_void_p(c_ci.data_ptr()), ias.i32p),
+                     C.cast(C.c_void_p(c_va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
+        rep = ias.Report()
+        rep_s = ias.Report()
 
-    def step_twophase():
-        n = C.c_int64(0)
-        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None,
-                                              C.byref(rep_s)), "nnz")
-        Cm.nnz = cap
-        ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
-                                                  C.byref(rep)), "compute")
-        rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
-        return rep
+        def step_onepass():
+            Cm.nnz = cap
+            ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
+                                                   C.byref(rep)), "into")
+            return rep
 
-    step = step_onepass if args.engine == "onepass" else step_twophase
+        def step_twophase():
+            n = C.c_int64(0)
+            ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(n), None,
+                                                  C.byref(rep_s)), "nnz")
+            Cm.nnz = cap
+            ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
+                                                      C.byref(rep)), "compute")
+            rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
+            return rep
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    reps = []
-    for _ in range(args.steps):
-        r = step()
-        reps.append((r.ms_total, r.ms_analysis, r.ms_symbolic, r.ms_numeric, r.ms_stream))
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    local_nnz = int(Cm.nnz) if args.engine == "onepass" else cap
-    nnz_tot = torch.tensor([float(local_nnz)], dtype=torch.float64, device=dev)
-    num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
-    if dist_on:
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(nnz_tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(num_ms, op=dist.ReduceOp.MAX)
-    elapsed = float(t_max.item())
-    ms_step = 1000.0 * elapsed / args.steps
-    gflops = 2.0 * flops_total / (ms_step * 1e6)
-    nnz_c_total = int(nnz_tot.item())
+        step = step_onepass if args.engine == "onepass" else step_twophase
 
-    # Roofline (HBM-bound).  Dominant launch: k_numeric_flat
-    # (k_onepass for --engine onepass), event-timed on its own stream inside
-    # the library.  Its algorithmic bytes per launch follow §8(d3)'s B_alg:
-    # the C entries it writes (12 B each) plus one read of A and of B
-    # (bytes(X) = 8·(rows+1) + 12·nnz(X)); the B-row re-reads (12 B per
-    # product, mostly served by L2 / the Infinity Cache) are reported
-    # separately as gather_bytes, never in `achieved`.
-    rows_local = r1 - r0
-    bytes_a = 8 * (rows_local + 1) + 12 * int(Am.nnz)
-    bytes_b = 8 * (rows + 1) + 12 * nnz_a
-    bytes_c = 8 * (rows_local + 1) + 12 * local_nnz
-    alg_bytes = bytes_a + bytes_b + bytes_c
-    ms_flat = statistics.mean(x[4] for x in reps)
-    flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
-    gather_bytes = 12 * int(rep.stream_products)
-    achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
-    kname = "k_onepass" if args.engine == "onepass" else "k_numeric_flat"
-    traffic, lds_conf = None, None
-    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
-    if os.path.exists(pmc_file):
-        try:
-            prof = json.load(open(pmc_file))
-            traffic = prof.get(kname, {}).get("hbm_bytes_per_launch")
-            lds_conf = prof.get("lds_bank_conflict_ratio")
-        except Exception:
-            traffic, lds_conf = None, None
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = []
+        for _ in range(args.steps):
+            r = step()
+            reps.append((r.ms_total, r.ms_analysis, r.ms_symbolic, r.ms_numeric, r.ms_stream))
+        torch.cuda.synchronize()
+        if dist_on:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        local_nnz = int(Cm.nnz) if args.engine == "onepass" else cap
+        nnz_tot = torch.tensor([float(local_nnz)], dtype=torch.float64, device=dev)
+        num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
+        if dist_on:
+            dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+            dist.all_reduce(nnz_tot, op=dist.ReduceOp.SUM)
+            dist.all_reduce(num_ms, op=dist.ReduceOp.MAX)
+        elapsed = float(t_max.item())
+        ms_step = 1000.0 * elapsed / args.steps
+        gflops = 2.0 * flops_total / (ms_step * 1e6)
+        nnz_c_total = int(nnz_tot.item())
 
-    out = {
-        "metric": METRIC,
-        "value": round(gflops, 3),
-        "unit": "GFLOP/s",
-        "n_gpus": world_req,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (deterministic R-MAT/band/ELL generator, ia-spgemm_amd/csrc/gen.cpp)",
-        "config": {
-            "workload": desc,
-            "kind": kind, **prm,
-            "rows": rows, "nnz_a": nnz_a, "flops": flops_total, "nnz_c": nnz_c_total,
-            "order": args.order,
-            "engine": args.engine,
-            "parallelism": f"row-block x{world_req}, B replicated",
-        },
-        "nnz_per_s": round(nnz_c_total / (ms_step * 1e-3), 1),
-        "phases_ms_rank0": {
-            "total_device": round(statistics.mean(x[0] for x in reps), 4),
-            "analysis": round(statistics.mean(x[1] for x in reps), 4),
-            "symbolic": round(statistics.mean(x[2] for x in reps), 4),
-            "numeric": round(statistics.mean(x[3] for x in reps), 4),
-        },
-        "roofline": {
-            "kernel": kname,
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "alg_bytes_per_launch": flat_bytes,
-            "alg_bytes_formula": "12*c_entries + bytes(A) + bytes(B), bytes(X) = 8*(rows+1) + 12*nnz(X)",
-            "gather_bytes": gather_bytes,
-            "lds_bank_conflict_ratio": lds_conf,
-            "ms_per_launch": round(ms_flat, 4),
-            "units_per_launch": {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)},
-        },
-        "roofline_step": {
-            "what": "whole step: B_alg = bytes(A) + bytes(B) + bytes(C) (SURVEY 8 d3) / step time",
-            "alg_bytes": alg_bytes,
-            "achieved": round(alg_bytes / (ms_step * 1e-3) / 1e9, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-        },
-        "setup_s": round(t_gen, 2),
-    }
+        # Roofline (SURVEY §8 d3, HBM-bound).  Dominant launch: the streaming
+        # numeric pass (k_num2; k_onepass for --engine onepass), event-timed on
+        # its own stream inside the library.  Its algorithmic bytes per launch
+        # follow §8(d3)'s B_alg: the C entries it writes (12 B each) plus one
+        # read of A and of B (bytes(X) = 8·(rows+1) + 12·nnz(X)); the B-row
+        # re-reads (12 B per product, mostly served by L2 / the Infinity Cache)
+        # are reported separately as gather_bytes, never in `achieved`.
+        rows_local = r1 - r0
+        bytes_a = 8 * (rows_local + 1) + 12 * int(Am.nnz)
+        bytes_b = 8 * (rows + 1) + 12 * nnz_a
+        bytes_c = 8 * (rows_local + 1) + 12 * local_nnz
+        alg_bytes = bytes_a + bytes_b + bytes_c
+        ms_flat = statistics.mean(x[4] for x in reps)
+        flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
+        gather_bytes = 12 * int(rep.stream_products)
+        achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
+        kname = "k_onepass" if args.engine == "onepass" else \
+            ("k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2")
+        traffic, lds_conf = None, None
+        pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
+        if os.path.exists(pmc_file):
+            try:
+                prof = json.load(open(pmc_file))
+                traffic = prof.get(kname, {}).get("hbm_bytes_per_launch")
+                lds_conf = prof.get("lds_bank_conflict_ratio")
+            except Exception:
+                traffic, lds_conf = None, None
 
-    if args.as_rank is not None and not dist_on:
-        out["as_rank"] = {"rank": args.as_rank, "of": world_req, "rows": [r0, r1],
-                          "note": "one rank's shard only: value / nnz_per_s are per-rank figures"}
-        shard_flops = int(rep_s.flops) if args.engine == "twophase" else int(rep.flops)
-        out["as_rank"]["flops"] = shard_flops
-        out["value"] = round(2.0 * shard_flops / (ms_step * 1e6), 3)
-        out["n_gpus"] = 1
-    if rank == 0 and world == 1 and args.as_rank is None and not args.no_cpu_baseline and \
-            kind in ("rmat", "band", "ell"):
-        out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
-        if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
-            out["speedup_vs_cpu_baseline"] = round(gflops / out["cpu_baseline"]["value"], 2)
-        out["cpu_baseline_alg2"] = cpu_baseline_alg2(A, flops_total, args.cpu_threads)
-
-    if rank == 0 and world == 1 and args.as_rank is None and not args.no_host_e2e:
-        # the end-to-end rate with host operands (A, B uploaded, C
-        # downloaded over PCIe inside the call), one call after the timed
-        # region; never `value`.
-        del c_ci, c_va
-        torch.cuda.empty_cache()
-        t_e = time.perf_counter()
-        _, rh = ias.spgemm(A, order=order, device=local)
-        wall = (time.perf_counter() - t_e) * 1e3
-        out["host_e2e"] = {
-            "what": "one ias_csr_mul_csr call with host A, B and host C (upload + compute + download); "
-                    "ms_wall also holds the call's workspace allocation and the numpy copy of C",
-            "ms_wall": round(wall, 2), "ms_upload": round(rh.ms_upload, 3),
-            "ms_device": round(rh.ms_total, 3), "ms_download": round(rh.ms_download, 3),
-            "gflops_pcie_inclusive": round(2.0 * flops_total / (wall * 1e6), 3),
+        out = {
+            "metric": METRIC,
+            "value": round(gflops, 3),
+            "unit": "GFLOP/s",
+            "n_gpus": world_req,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (deterministic R-MAT/band/ELL generator, ia-spgemm_amd/csrc/gen.cpp)",
+            "config": {
+                "workload": desc,
+                "kind": kind, **prm,
+                "rows": rows, "nnz_a": nnz_a, "flops": flops_total, "nnz_c": nnz_c_total,
+                "order": args.order,
+                "engine": args.engine,
+                "parallelism": f"row-block x{world_req}, B replicated",
+            },
+            "nnz_per_s": round(nnz_c_total / (ms_step * 1e-3), 1),
+            "phases_ms_rank0": {
+                "total_device": round(statistics.mean(x[0] for x in reps), 4),
+                "analysis": round(statistics.mean(x[1] for x in reps), 4),
+                "symbolic": round(statistics.mean(x[2] for x in reps), 4),
+                "numeric": round(statistics.mean(x[3] for x in reps), 4),
+            },
+            "roofline": {
+                "kernel": kname,
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": flat_bytes,
+                "alg_bytes_formula": "12*c_entries + bytes(A) + bytes(B), bytes(X) = 8*(rows+1) + 12*nnz(X)",
+                "gather_bytes": gather_bytes,
+                "lds_bank_conflict_ratio": lds_conf,
+                "ms_per_launch": round(ms_flat, 4),
+                "units_per_launch": {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)},
+            },
+            "roofline_step": {
+                "what": "whole step: B_alg = bytes(A) + bytes(B) + bytes(C) (SURVEY 8 d3) / step time",
+                "alg_bytes": alg_bytes,
+                "achieved": round(alg_bytes / (ms_step * 1e-3) / 1e9, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(alg_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            },
+            "setup_s": round(t_gen, 2),
         }
+        if as_ranks is not None:
+            out["as_rank"] = {"rank": shard, "of": world_req, "rows": [r0, r1],
+                              "note": "one rank's shard only: value / nnz_per_s are per-rank figures"}
+            shard_flops = int(rep_s.flops) if args.engine == "twophase" else int(rep.flops)
+            out["as_rank"]["flops"] = shard_flops
+            out["as_rank"]["nnz_c"] = local_nnz
+            out["value"] = round(2.0 * shard_flops / (ms_step * 1e6), 3)
+            out["nnz_per_s"] = round(local_nnz / (ms_step * 1e-3), 1)
+            out["n_gpus"] = 1
+        return out, step, (c_rp, c_ci[:local_nnz], c_va[:local_nnz])
+
+    shards = as_ranks if as_ranks is not None else [rank]
+    for shard in shards:
+        out, step, cbufs = run_shard(shard)
+        if dist_on and not args.no_gather:
+            out["allgatherv"] = measure_allgatherv(step, *cbufs, args.gather_reps)
+        if rank == 0 and world == 1 and as_ranks is None and not args.no_cpu_baseline and \
+                kind in ("rmat", "band", "ell"):
+            out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
+            if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
+                out["speedup_vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+            out["cpu_baseline_alg2"] = cpu_baseline_alg2(A, flops_total, args.cpu_threads)
+
+        if rank == 0 and world == 1 and as_ranks is None and not args.no_host_e2e:
+            # SURVEY 8 d1: the end-to-end rate with host operands (A, B uploaded, C
+            # downloaded over PCIe inside the call), one call after the timed
+            # region; never `value`.
+            del cbufs, step
+            torch.cuda.empty_cache()
+            step = cbufs = None
+            t_e = time.perf_counter()
+            _, rh = ias.spgemm(A, order=order, device=local)
+            wall = (time.perf_counter() - t_e) * 1e3
+            out["host_e2e"] = {
+                "what": "one ias_csr_mul_csr call with host A, B and host C (upload + compute + download); "
+                        "ms_wall also holds the call's workspace allocation and the numpy copy of C",
+                "ms_wall": round(wall, 2), "ms_upload": round(rh.ms_upload, 3),
+                "ms_device": round(rh.ms_total, 3), "ms_download": round(rh.ms_download, 3),
+                "gflops_pcie_inclusive": round(2.0 * flops_total / (wall * 1e6), 3),
+            }
+        if rank == 0:
+            line = json.dumps(out)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "a" if len(shards) > 1 else "w") as f:
+                    f.write(line + "\n")
+        del cbufs, step
+        torch.cuda.empty_cache()
 
     ias.lib.ias_plan_destroy(plan)
-    if rank == 0:
-        line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
-                f.write(line + "\n")
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def measure_allgatherv(step, c_rp, c_ci, c_va, reps=1):
+    """SURVEY §8 e1's exchange step, after the timed loop: `reps` times one
+    step compute-only and one step compute + the allgatherv that concatenates
+    the row-sharded C on every rank (ias/dist.py gather_csr: per-rank counts,
+    then one RCCL broadcast per root into that root's slice), each bracketed by
+    barriers, max over ranks.  Returns ms figures and the bytes each rank
+    receives."""
+    import torch
+    import torch.distributed as dist
+    from ias.dist import gather_csr
+    dev = c_ci.device
+    sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
+
+    def timed(fn):
+        sync()
+        dist.barrier()
+        sync()
+        t = time.perf_counter()
+        res = fn()
+        sync()
+        dist.barrier()
+        sync()
+        el = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        return 1e3 * float(el.item()), res
+
+    def compute_and_gather():
+        step()
+        return gather_csr(c_rp, c_ci, c_va, mode="all")
+
+    mc, mcg = [], []
+    full_nnz = full_rows = 0
+    for _ in range(max(1, reps)):
+        ms, _ = timed(step)
+        mc.append(ms)
+        ms, full = timed(compute_and_gather)
+        mcg.append(ms)
+        full_rows, full_nnz = int(full[0].numel()) - 1, int(full[1].numel())
+        del full
+    rows_local, nnz_local = int(c_rp.numel()) - 1, int(c_ci.numel())
+    rv = torch.tensor([12 * (full_nnz - nnz_local) + 8 * (full_rows - rows_local)], dtype=torch.int64, device=dev)
+    dist.all_reduce(rv, op=dist.ReduceOp.MAX)
+    recv = int(rv.item())
+    ms_c, ms_cg = min(mc), min(mcg)
+    ms_g = max(ms_cg - ms_c, 1e-6)
+    return {"what": "one step compute-only vs compute + RCCL allgatherv of C on every rank "
+                    "(ias/dist.py gather_csr), max over ranks, best of reps",
+            "reps": max(1, reps), "ms_compute": round(ms_c, 3), "ms_compute_allgatherv": round(ms_cg, 3),
+            "ms_allgatherv": round(ms_g, 3), "c_nnz_total": full_nnz,
+            "bytes_received_per_rank_max": recv,
+            "gbps_received_per_rank": round(recv / (ms_g * 1e-3) / 1e9, 1)}
 
 
 def row_sample(A, every):

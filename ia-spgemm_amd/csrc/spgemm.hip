@@ -2335,10 +2335,8 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     auto lst = [&](int b) { return lists + st[b]; };
     // wide rows: compact radix workspace (their entries, scanned), else the
     // padded per-row bitonic workspace (12 B per binning slot)
-    static const bool force_global = [] {
-        const char *e = getenv("IAS_SORT_GLOBAL");
-        return e && *e == '1';
-    }();
+    const char *fg = getenv("IAS_SORT_GLOBAL");   // read per call: a test knob
+    const bool force_global = fg && *fg == '1';
     bool radix = false;
     size_t rtmp = 0, slots = 0;
     int64_t *coff = nullptr;

@@ -28,12 +28,13 @@ def need_gpu():
         pytest.fail("no HIP device visible: the gpu tests must run on an MI355X box")
 
 
-@pytest.fixture(params=["onepass", "twophase"], autouse=True)
-def engine(request, monkeypatch):
-    """Every case runs through both CSR engines: the single-pass chunk engine
-    (IAS_ONEPASS=1) and the two-phase engine (the default)."""
-    monkeypatch.setenv("IAS_ONEPASS", "1" if request.param == "onepass" else "0")
-    return request.param
+@pytest.fixture(autouse=True)
+def engine(monkeypatch):
+    """Every case runs through the two-phase engine (the default); the opt-in
+    single-pass chunk engine (IAS_ONEPASS=1) has its own cases below
+    (test_onepass_engine_*)."""
+    monkeypatch.setenv("IAS_ONEPASS", "0")
+    return "twophase"
 
 
 def bits(a):
@@ -633,3 +634,114 @@ def test_host_operand_transfer_times():
         ias.lib.ias_csr_free(C.byref(c))
     finally:
         ias.lib.ias_csr_free(C.byref(dA))
+
+
+# ------------------------------------------------------------------ opt-in single-pass engine
+@pytest.mark.parametrize("name", SQUARE)
+def test_onepass_engine_inputs(inputs_dir, name, monkeypatch):
+    monkeypatch.setenv("IAS_ONEPASS", "1")
+    A = ias.mtx_read(os.path.join(inputs_dir, name))
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, _ = ias.spgemm(A)
+    assert_csr_identical(got, ref, name + " (onepass)")
+
+
+@pytest.mark.parametrize("case", cases_small()[:4], ids=lambda c: c[0])
+def test_onepass_engine_synthetic(case, monkeypatch):
+    monkeypatch.setenv("IAS_ONEPASS", "1")
+    name, A, _ = case
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+    got, _ = ias.spgemm(A)
+    assert_csr_identical(got, ref, name + " (onepass)")
+
+
+# ------------------------------------------------------------------ sorted order, wide rows
+def many_wide_rows(rows=40000, n=40000, nwide=60, mmax=230, seed=9):
+    """A*B with `nwide` rows of A whose C rows hold ~2000-20000 entries
+    (radix-sort segments of different sizes with short rows between them);
+    B rows ~100 entries, the other A rows 0-3 entries."""
+    rng = np.random.default_rng(seed)
+    wide = set(rng.choice(rows, nwide, replace=False).tolist())
+    arows = []
+    for i in range(rows):
+        m = int(rng.integers(22, mmax)) if i in wide else int(rng.integers(0, 4))
+        arows.append(np.sort(rng.choice(n, m, replace=False)))
+    brows = [np.sort(rng.choice(n, int(rng.integers(80, 120)), replace=False)) for _ in range(n)]
+
+    def mk(rs):
+        rp = np.zeros(len(rs) + 1, np.int64)
+        rp[1:] = np.cumsum([len(r) for r in rs])
+        col = np.concatenate(rs).astype(np.int32)
+        val = rng.standard_normal(col.size)
+        return ias.HostCsr(len(rs), n, rp, col, val)
+
+    return mk(arows), mk(brows)
+
+
+def _wide_rows_ref():
+    A, B = many_wide_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    nnz_row = np.diff(ref.row_ptr)
+    assert ((nnz_row > 2048) & (nnz_row <= 20000)).sum() >= 40 and nnz_row.max() > 8192
+    return A, B, ref
+
+
+@pytest.mark.parametrize("force_global", ["0", "1"])
+def test_sorted_wide_rows_csr(force_global, monkeypatch):
+    """Rows past the LDS sort bins: the segmented radix sort (default) and
+    the per-row bitonic workspace (IAS_SORT_GLOBAL=1)."""
+    monkeypatch.setenv("IAS_SORT_GLOBAL", force_global)
+    A, B, ref = _wide_rows_ref()
+    got, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+    rc, rv = sorted_form(ref)
+    np.testing.assert_array_equal(got.row_ptr, ref.row_ptr)
+    np.testing.assert_array_equal(got.col, rc)
+    np.testing.assert_array_equal(bits(got.val), bits(rv))
+
+
+@pytest.mark.parametrize("force_global", ["0", "1"])
+def test_sorted_wide_rows_coo(force_global, monkeypatch):
+    monkeypatch.setenv("IAS_SORT_GLOBAL", force_global)
+    A, B = many_wide_rows()
+    ref, ref_rows = ob.coo_mul_coo(ob.Mat.of(A), ob.Mat.of(B))
+    ca, cb, cc = _coo_of(A), _coo_of(B), ias.Coo()
+    o = ias.opts(order=ias.ORDER_SORTED, output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_coo_mul_coo(C.byref(ca), C.byref(cb), C.byref(cc), C.byref(o), None), "coo")
+    n = cc.nnz
+    got_r = ias._np(cc.row, n, np.int32)
+    got_c = ias._np(cc.col, n, np.int32)
+    got_v = ias._np(cc.val, n, np.float64)
+    for m in (ca, cb, cc):
+        ias.lib.ias_coo_free(C.byref(m))
+    rc, rv = sorted_form(ref)
+    np.testing.assert_array_equal(got_r, ref_rows)
+    np.testing.assert_array_equal(got_c, rc)
+    np.testing.assert_array_equal(bits(got_v), bits(rv))
+
+
+@pytest.mark.parametrize("force_global", ["0", "1"])
+def test_sorted_wide_rows_ell(force_global, monkeypatch):
+    """ELL output: the sort spans (row * K, nnz_row) instead of row pointers."""
+    monkeypatch.setenv("IAS_SORT_GLOBAL", force_global)
+    A, B = many_wide_rows(rows=1000, n=30000, nwide=40, mmax=130)   # C: 1000 x K<=13000 padded
+    ref = ob.ell_mul_ell(ob.Mat.of(A), ob.Mat.of(B))
+    assert (ref["nnz_row"] > 2048).sum() >= 25
+    sa, sb = A.struct(), B.struct()
+    ea, eb, ec = ias.Ell(), ias.Ell(), ias.Ell()
+    ias.check(ias.lib.ias_csr_to_ell(C.byref(sa), C.byref(ea), 0.0), "to_ell")
+    ias.check(ias.lib.ias_csr_to_ell(C.byref(sb), C.byref(eb), 0.0), "to_ell")
+    o = ias.opts(order=ias.ORDER_SORTED, output_memory=ias.MEMORY_HOST)
+    ias.check(ias.lib.ias_ell_mul_ell(C.byref(ea), C.byref(eb), C.byref(ec), C.byref(o), None), "ell")
+    K = ec.max_nnz_per_row
+    assert K == ref["K"]
+    got_n = ias._np(ec.nnz_row, ec.rows, np.int32)
+    got_c = ias._np(ec.col, ec.rows * K, np.int32).reshape(ec.rows, K)
+    got_v = ias._np(ec.val, ec.rows * K, np.float64).reshape(ec.rows, K)
+    for m in (ea, eb, ec):
+        ias.lib.ias_ell_free(C.byref(m))
+    np.testing.assert_array_equal(got_n, ref["nnz_row"])
+    for i in np.nonzero(got_n)[0]:
+        k = got_n[i]
+        o_ = np.argsort(ref["col"][i, :k], kind="stable")
+        np.testing.assert_array_equal(got_c[i, :k], ref["col"][i, :k][o_], err_msg=f"row {i}")
+        np.testing.assert_array_equal(bits(got_v[i, :k]), bits(ref["val"][i, :k][o_]), err_msg=f"row {i}")
