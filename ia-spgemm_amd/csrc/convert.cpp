@@ -351,12 +351,13 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
     IAS_TRY(HB.get(B));
     const ias_csr *a = HA.m, *b = HB.m;
     // Estimated device cost per row, in tenths of a product: a fixed cost per
-    // row (binning, launch share) plus its products, those of rows beyond
-    // the LDS bins (hash-partitioned, > 10922 products) weighted 2.1x.
-    // Calibrated on MI355X from K3' and two ranks of the 8-GPU scale-23 run
-    // (15.6 ps per product, 33 ps per partitioned-row product, 0.57 ns per row;
-    // DESIGN.md §6), so the rank holding R-MAT's hub rows gets fewer of them.
-    constexpr int64_t ROW_COST = 370, SMALL = 10, BIG = 21, PART_MIN = 10922;
+    // row (binning, per-row passes, launch share) plus its products, those of
+    // rows beyond the LDS bins (hash-partitioned, > 16384 products) weighted
+    // 3.4x.  Calibrated on MI355X (non-negative least squares over K3' and the
+    // eight rank shards of K4 run one at a time, bench.py --as-rank all:
+    // 1.78 ns per row, 10.4 ps per product, +25.2 ps per partitioned-row
+    // product), so the rank holding R-MAT's hub rows gets fewer.
+    constexpr int64_t ROW_COST = 1710, SMALL = 10, BIG = 34, PART_MIN = 16384;
     std::vector<int64_t> pref((size_t)a->rows + 1, 0);
     for (int64_t i = 0; i < a->rows; ++i) {
         int64_t prod = 0;

@@ -640,7 +640,7 @@ def test_host_operand_transfer_times():
 @pytest.mark.parametrize("name", SQUARE)
 def test_onepass_engine_inputs(inputs_dir, name, monkeypatch):
     monkeypatch.setenv("IAS_ONEPASS", "1")
-    A = ias.mtx_read(os.path.join(inputs_dir, name))
+    A, _ = ias.mtx_read(os.path.join(inputs_dir, name))
     ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
     got, _ = ias.spgemm(A)
     assert_csr_identical(got, ref, name + " (onepass)")
