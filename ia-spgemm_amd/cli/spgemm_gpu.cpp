@@ -6,14 +6,20 @@
 //   1 IAS row-wise hash, reference order (byte-identical to CSR_MUL_CSR)
 //   2 IAS row-wise hash + per-row sort (sorted columns, as csrgemm emits)
 // Usage: spgemm-gpu A.mtx [--aat] [--rand10] [--seed N] [--mtx-out C.mtx]
+//                        [--gpus N | --devices d0,d1,...]
 //   default C = A*A (the README's contract); --aat builds B = A^T on the
 //   device, as main.cu:260-269 does with mkl_dcsrcsc; --rand10 replaces
 //   values by rand()%10 as main.cu:236-243, seeded by --seed (the reference
-//   seeds with time(NULL)).
+//   seeds with time(NULL)).  --gpus N / --devices: A's rows split over N
+//   devices (ias_csr_mul_csr_multi: one host thread + plan per device, B on
+//   every device, C concatenated in row order; a device may repeat, which
+//   rehearses the split on one GPU); run_time = the slowest device.
 #include "ias.h"
 #include "report.hpp"
 
 #include <cstring>
+#include <string>
+#include <vector>
 
 using cli::AlgResult;
 
@@ -21,11 +27,25 @@ int main(int argc, char **argv) {
     const char *file = nullptr, *out_path = nullptr;
     bool aat = false, rand10 = false;
     unsigned seed = 0;
+    std::vector<int32_t> devices;
     for (int i = 1; i < argc; ++i) {
         if (!strcmp(argv[i], "--aat")) aat = true;
         else if (!strcmp(argv[i], "--rand10")) rand10 = true;
         else if (!strcmp(argv[i], "--seed") && i + 1 < argc) seed = (unsigned)atoi(argv[++i]);
         else if (!strcmp(argv[i], "--mtx-out") && i + 1 < argc) out_path = argv[++i];
+        else if (!strcmp(argv[i], "--gpus") && i + 1 < argc) {
+            devices.clear();
+            for (int d = 0, n = atoi(argv[++i]); d < n; ++d) devices.push_back(d);
+        } else if (!strcmp(argv[i], "--devices") && i + 1 < argc) {
+            devices.clear();
+            std::string l = argv[++i];
+            for (size_t p = 0; p <= l.size();) {
+                size_t q = l.find(',', p);
+                if (q == std::string::npos) q = l.size();
+                if (q > p) devices.push_back((int32_t)atoi(l.substr(p, q - p).c_str()));
+                p = q + 1;
+            }
+        }
         else if (!file) file = argv[i];
     }
     if (!file) {
@@ -65,9 +85,28 @@ int main(int argc, char **argv) {
     o.device = 0;
     CLI_TRY("plan", ias_plan_create(&o.plan, 0, nullptr));
     std::vector<AlgResult> r(2);
+    const bool multi = devices.size() > 1;
+    if (multi) std::printf("row blocks over %zu devices\n", devices.size());
     for (int alg = 0; alg < 2; ++alg) {
         o.order = alg == 0 ? IAS_ORDER_REFERENCE : IAS_ORDER_SORTED;
         ias_csr C{};
+        if (multi) {
+            ias_opts om = o;
+            om.plan = nullptr;
+            om.output_memory = IAS_MEMORY_HOST;
+            CLI_TRY("spgemm", ias_csr_mul_csr_multi(&dA, &dB, &C, (int32_t)devices.size(), devices.data(), &om,
+                                                    nullptr));   // warm-up
+            ias_csr_free(&C);
+            ias_report rep{};
+            CLI_TRY("spgemm", ias_csr_mul_csr_multi(&dA, &dB, &C, (int32_t)devices.size(), devices.data(), &om,
+                                                    &rep));
+            r[alg].run_ms = rep.ms_total;
+            r[alg].mem = ias_sizeof_csr(&C);
+            ias_sum_csr(&C, &r[alg].sum);
+            if (alg == 0 && out_path) CLI_TRY("write", ias_mtx_write(out_path, &C));
+            ias_csr_free(&C);
+            continue;
+        }
         CLI_TRY("spgemm", ias_csr_mul_csr(&dA, &dB, &C, &o, nullptr));   // warm-up
         ias_csr_free(&C);
         ias_report rep{};

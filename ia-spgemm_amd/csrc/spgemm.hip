@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <map>
 #include <mutex>
+#include <set>
 #include <tuple>
 #include <vector>
 
@@ -1451,10 +1452,18 @@ static BinSpec num_spec() {
 // the callers below are templates, so each has its own flag).
 template <typename F>
 static void allow_lds(F kernel, bool &done, size_t bytes) {
-    if (!done && bytes > 65536) {
+    (void)done;
+    if (bytes <= 65536) return;
+    // once per kernel and device; thread-safe (ias_csr_mul_csr_multi runs one
+    // host thread per device)
+    static std::mutex mu;
+    static std::set<std::pair<const void *, int>> seen;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    if (seen.insert({(const void *)kernel, dev}).second) {
         hipFuncSetAttribute((const void *)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipGetLastError();   // a refusal shows up at launch
-        done = true;
     }
 }
 

@@ -305,13 +305,42 @@ ias_status ias_csr_row_view(const ias_csr *A, int64_t r0, int64_t r1, ias_csr *v
 /* Split A's rows into nparts contiguous blocks of near-equal estimated device
  * cost (a flops prefix, not rows; each row weighted by a fixed
  * per-row cost plus its products, products of hash-partitioned rows counted
- * 2.1x, calibrated on MI355X); bounds has nparts+1 entries.
+ * 3.4x, calibrated on MI355X); bounds has nparts+1 entries.
  * Host or device A. */
 ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int32_t nparts,
                               int64_t *bounds);
 /* Add `offset` to every entry of a device row pointer (allgatherv fix-up). */
 ias_status ias_row_ptr_shift(int64_t *row_ptr, int64_t count, int64_t offset,
                              int32_t device, void *stream);
+
+/* One process, N devices (the reference is single-device, its
+ * CPU kernels split rows the same way over OpenMP threads,
+ * csr/common_csr.h:95-189): A's rows split by ias_partition_rows, one host
+ * thread + plan per device computes its block of C = A*B (host or device
+ * operands; B staged on every device), the blocks concatenated in row order
+ * into C (library-allocated; opts->output_memory host (default) or device =
+ * devices[0]).  devices may be NULL (0..ndev-1); a device may repeat.
+ * report: flops / nnz summed, times = the slowest device. */
+ias_status ias_csr_mul_csr_multi(const ias_csr *A, const ias_csr *B, ias_csr *C, int32_t ndev,
+                                 const int32_t *devices, const ias_opts *opts, ias_report *report);
+
+/* One process per GPU over RCCL (xGMI).  librccl is opened at first use.
+ * ias_dist_unique_id: rank 0 makes the id (>= 128 bytes) and shares it out of
+ * band; every rank then calls ias_dist_create with it. */
+typedef struct ias_dist ias_dist;
+ias_status ias_dist_unique_id(char *id, int32_t id_len);
+ias_status ias_dist_create(ias_dist **dist, const char *id, int32_t nranks, int32_t rank, int32_t device);
+ias_status ias_dist_destroy(ias_dist *dist);
+/* Concatenate the row-sharded C on every rank: C_local (device, this rank's
+ * rows, row pointer from 0) -> C_full (library-allocated on the rank's
+ * device): per-rank counts by ncclAllGather, then one ncclBroadcast per root
+ * into its slice (one group), row pointers shifted by the global nnz offset. */
+ias_status ias_dist_allgatherv_csr(ias_dist *dist, const ias_csr *C_local, ias_csr *C_full, void *stream);
+/* This rank's row block of C = A*B (A, B replicated, host or device): C is the
+ * block (gather = 0) or the whole C on every rank (gather = 1), on the rank's
+ * device, library-allocated. */
+ias_status ias_dist_csr_mul_csr(ias_dist *dist, const ias_csr *A, const ias_csr *B, ias_csr *C,
+                                int32_t gather, int32_t order, ias_report *report);
 
 /* ---------------------------------------------------------------- synthetic inputs
  * Deterministic host generators (counter-based splitmix64; identical on every

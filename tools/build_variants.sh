@@ -17,7 +17,7 @@ wait
 for v in "${VS[@]}"; do
   name=${v%%:*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build_var/libias_$name.so build_var/spgemm_$name.o \
-     $O/ias_api.o $O/dia.o $O/convert_dev.o $O/mtx_io.o $O/gen.o $O/convert.o $O/mkl_baseline.o $O/matnet.o \
+     $O/ias_api.o $O/multi.o $O/dia.o $O/convert_dev.o $O/mtx_io.o $O/gen.o $O/convert.o $O/mkl_baseline.o $O/matnet.o \
      -L/usr/lib/gcc/x86_64-linux-gnu/11 -lgomp -ldl
   echo "built build_var/libias_$name.so"
 done
