@@ -7,6 +7,7 @@
 #include "onepass_kernels.hpp"
 #include "sym2_kernels.hpp"
 #include "num2_kernels.hpp"
+#include "short_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
 
@@ -32,10 +33,12 @@ __device__ __forceinline__ uint32_t nparts_of(int32_t key, int32_t cap) {
 // stv: the row's streaming state (-2: none given; >= 0: a streaming row with
 // stv duplicates -> the fix-up bin when it has any, nothing to do otherwise;
 // -3: a table-path row without a first-touch bitmap too long for the LDS
-// bins -> the per-row global table).
+// bins -> the per-row global table; -5: a short row (<= SHORT_MAX products,
+// short_kernels.hpp) -> its numeric bin by products).
 __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod, int32_t stv, int32_t ent2 = 0) {
     if (k <= 0) return 0;
     if (stv == -3) return sp.nval + 2;
+    if (stv == -5 && sp.short_base > 0) return sp.short_base + (prod <= 64 ? 0 : (prod <= 128 ? 1 : 2));
     if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), longer (sorted)
         if (stv == 0) return 0;
         return sp.nval + 3 + sp.ndw + (stv > 256 ? 2 : (stv > 16 ? 1 : 0));
@@ -1445,7 +1448,23 @@ static BinSpec num_spec() {
     s.wide_min = WIDE_MIN;
     s.ft = 0;
     s.zero_nnz = 0;
+    s.short_base = N_VAL + 3 + N_DW + 3;   // after the fix-up bins
     return s;
+}
+static_assert(N_VAL + 3 + N_DW + 3 + 3 <= MAX_BINS, "short bins beyond MAX_BINS");
+
+// Rows of at most SHORT_MAX products take the short path (short_kernels.hpp:
+// one wave per row, exact LDS table, no bitmap) in both passes; IAS_SHORT=0
+// sends them through sym2 + the streaming numeric pass instead.
+#ifndef SHORT_MAX
+#define SHORT_MAX 256
+#endif
+static bool short_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SHORT");
+        return !(e && *e == '0');
+    }();
+    return on;
 }
 
 // Dynamic LDS beyond 64 KiB is requested per kernel (once per instantiation:
@@ -1491,6 +1510,31 @@ static int64_t resident_blocks(F kernel, int threads, size_t lds) {
     std::lock_guard<std::mutex> g(mu);
     cache[key] = v;
     return v;
+}
+
+// One wave per row (the kernels' grid-stride loop then runs once): measured
+// faster than persistent waves capped at the resident count with the next
+// row prefetched (K2: 0.99 / 1.46 ms vs 1.16 / 1.56 ms symbolic / numeric).
+// IAS_SHORT_PERSIST=1 caps the grid at the resident workgroups instead.
+template <typename F>
+static unsigned short_grid(F kern, int32_t count) {
+    static const bool persist = [] {
+        const char *e = getenv("IAS_SHORT_PERSIST");
+        return e && *e == '1';
+    }();
+    const int64_t want = (count + SH_WPB - 1) / SH_WPB;
+    if (!persist) return (unsigned)std::max<int64_t>(1, want);
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, resident_blocks(kern, 64 * SH_WPB, 0)));
+}
+static void short_sym_launch(int32_t upper, const ShortArgs &a, hipStream_t t) {
+    if (upper <= 64) k_short_sym<1><<<short_grid(k_short_sym<1>, a.count), 64 * SH_WPB, 0, t>>>(a);
+    else if (upper <= 128) k_short_sym<2><<<short_grid(k_short_sym<2>, a.count), 64 * SH_WPB, 0, t>>>(a);
+    else k_short_sym<4><<<short_grid(k_short_sym<4>, a.count), 64 * SH_WPB, 0, t>>>(a);
+}
+static void short_num_launch(int i, const ShortArgs &a, const Out &out, hipStream_t t) {
+    if (i == 0) k_short_num<1><<<short_grid(k_short_num<1>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
+    else if (i == 1) k_short_num<2><<<short_grid(k_short_num<2>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
+    else k_short_num<4><<<short_grid(k_short_num<4>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
 }
 
 // IAS_PART_BUCKET=0: partitioned rows rescan their expansion per partition
@@ -1926,6 +1970,12 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const char *e = getenv("IAS_S2_ABLATE");
                 return e ? atoi(e) : 0;
             }();
+            if (u <= SHORT_MAX && short_on()) {
+                const ShortArgs sh{A, ax, B.col, B.val, SL + st[b], c, nnz, sa.dupn};
+                short_sym_launch(u, sh, t);
+                CHECK_LAUNCH("k_short_sym", t);
+                continue;
+            }
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
                         sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl, DW_MAX};
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
@@ -2086,6 +2136,13 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             CHECK_LAUNCH("k_fixup_big", t);
         }
     }
+    for (int i = 2; i >= 0 && ns.short_base > 0; --i)
+        if ((c = num_count[ns.short_base + i]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            const ShortArgs sh{A, ax, B.col, B.val, NL + st[ns.short_base + i], c, nullptr, nullptr};
+            short_num_launch(i, sh, out, t);
+            CHECK_LAUNCH("k_short_num", t);
+        }
     for (int b = ns.nval; b >= 1; --b)
         if ((c = num_count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);

@@ -29,6 +29,8 @@ struct BinSpec {
     int32_t zero_nnz;          // write nnz_row = 0 for empty and partitioned rows
     int32_t ent_key;           // > 0: LDS bin i also needs ent_key * (A entries of the row) <= upper[i]
                                // (sym2 stages the row's entry bases in LDS, upper/ent_key of them)
+    int32_t short_base;        // > 0: rows marked short (stv -5) -> bins short_base + 0/1/2 by
+                               // products <= 64 / 128 / 256 (numeric pass of the short rows)
 };
 
 // Device-side counters, copied to the host after each binning.
