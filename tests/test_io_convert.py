@@ -179,8 +179,8 @@ def test_flops_sums_partition():
         rl = np.diff(A.row_ptr)
         prod = np.zeros(A.rows, np.int64)
         np.add.at(prod, np.repeat(np.arange(A.rows), rl), rl[A.col])
-        # the documented cost model (include/ias.h, convert.cpp): 370 per row +
-        # 10 per product, 21 per product of rows beyond 10922 products
-        cost = 370 + prod * np.where(prod > 10922, 21, 10)
+        # the documented cost model (include/ias.h, convert.cpp): 1710 per row +
+        # 10 per product, 34 per product of rows beyond 16384 products
+        cost = 1710 + prod * np.where(prod > 16384, 34, 10)
         w = [cost[bl[k]:bl[k + 1]].sum() for k in range(parts)]
         assert max(w) <= (sum(w) / parts) * 1.05 + cost.max() + 1
