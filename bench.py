@@ -43,7 +43,8 @@ HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
 CONFIGS = {
     # name: (kind, params, description)
-    "k1": ("band", dict(n=1 << 18, h=3, seed=7), "banded 256k x 256k, 7 diagonals (CSR path)"),
+    "k1": ("band", dict(n=1 << 18, h=3, seed=7), "banded 256k x 256k, 7 diagonals"),
+    "k1w": ("band", dict(n=1 << 18, h=32, seed=7), "banded 256k x 256k, 65 diagonals (wide band: DIA MFMA A/B)"),
     "k2": ("ell", dict(n=1 << 20, k=16, seed=7), "ELL-shaped 1M x 1M, 16 nnz/row (CSR path)"),
     "k3": ("rmat", dict(scale=20, ef=32, seed=1), "R-MAT 2^20, avg 32 nnz/row"),
     "k3p": ("rmat", dict(scale=20, ef=20, seed=2), "R-MAT 2^20, ~20 nnz/row (north-star headline)"),
@@ -68,6 +69,9 @@ def parse(argv=None):
                    help="single process: run only rank R's shard of the --gpus N workload "
                         "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers); "
                         "'R1,R2,...' or 'all' run several shards one after the other, one line each")
+    p.add_argument("--format", default="csr", choices=["csr", "dia"],
+                   help="dia: C = A*A through the DIA kernel (ias_dia_mul_dia) on device-resident DIA "
+                        "operands (banded configs, N=1)")
     p.add_argument("--no-gather", action="store_true", help="N>1: skip the allgatherv measurement")
     p.add_argument("--gather-reps", type=int, default=1, help="N>1: repetitions of the allgatherv measurement")
     return p.parse_args(argv)
@@ -170,6 +174,12 @@ def main(argv=None):
                        C.cast(C.c_void_p(ci.data_ptr()), ias.i32p),
                        C.cast(C.c_void_p(va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
 
+    if args.format == "dia":
+        if dist_on or as_ranks is not None:
+            raise SystemExit("--format dia runs on one GPU")
+        run_dia(args, A, kind, prm, desc, flops_total, local, t_gen)
+        return
+
     Bm = dcsr(0, rows, rp, nnz_a)
     plan = C.c_void_p()
     ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
@@ -271,9 +281,19 @@ def main(argv=None):
         ms_flat = statistics.mean(x[4] for x in reps)
         flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
         gather_bytes = 12 * int(rep.stream_products)
-        achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
         kname = "k_onepass" if args.engine == "onepass" else \
             ("k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2")
+        units = {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)}
+        if args.engine == "twophase" and int(rep.stream_nnz) < local_nnz // 2:
+            # most of C comes from the short-row / table kernels (K1, K2): the
+            # dominant unit is then the whole numeric phase (event-timed), its
+            # bytes the C entries it writes plus one read of A and B
+            kname = "numeric phase (k_short_num / table kernels)"
+            ms_flat = statistics.mean(x[3] for x in reps)
+            flat_bytes = 12 * local_nnz + bytes_a + bytes_b
+            gather_bytes = 12 * int(rep_s.flops)
+            units = {"products": int(rep_s.flops), "c_entries": local_nnz}
+        achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
         traffic, lds_conf = None, None
         pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
         if os.path.exists(pmc_file):
@@ -325,7 +345,7 @@ def main(argv=None):
                 "gather_bytes": gather_bytes,
                 "lds_bank_conflict_ratio": lds_conf,
                 "ms_per_launch": round(ms_flat, 4),
-                "units_per_launch": {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)},
+                "units_per_launch": units,
             },
             "roofline_step": {
                 "what": "whole step: B_alg = bytes(A) + bytes(B) + bytes(C) (SURVEY 8 d3) / step time",
@@ -390,6 +410,77 @@ def main(argv=None):
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
+    """One step = ias_dia_mul_dia(A, A) on device-resident DIA operands (C
+    allocated by the library on the device and freed after the step, as the
+    ABI hands it over); the kernel time is the call's event-timed ms_total."""
+    import torch
+    import ias
+    s = A.struct()
+    ha, da = ias.Dia(), ias.Dia()
+    ias.check(ias.lib.ias_csr_to_dia(C.byref(s), C.byref(ha), 0.0), "to_dia")
+    ias.check(ias.lib.ias_dia_copy(C.byref(ha), C.byref(da), ias.MEMORY_DEVICE, local), "dia upload")
+    nda = int(ha.num_diagonals)
+    ias.lib.ias_dia_free(C.byref(ha))
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
+    o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=local, plan=plan)
+    rep = ias.Report()
+    ndc = [0]
+
+    def step():
+        dc = ias.Dia()
+        ias.check(ias.lib.ias_dia_mul_dia(C.byref(da), C.byref(da), C.byref(dc), C.byref(o), C.byref(rep)), "dia")
+        ndc[0] = int(dc.num_diagonals)
+        ias.lib.ias_dia_free(C.byref(dc))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        step()
+        kms.append(rep.ms_total)
+    torch.cuda.synchronize()
+    ms_step = 1e3 * (time.perf_counter() - t0) / args.steps
+    ms_k = statistics.mean(kms)
+    rows = int(A.rows)
+    alg = 8 * rows * (2 * nda + ndc[0]) + 4 * (2 * nda + ndc[0])   # A, B (= A) read, C written
+    env = os.environ.get("IAS_DIA_MFMA")
+    mfma = env == "1" if env is not None else nda * nda >= 256   # the library's choice (dia.hip)
+    out = {
+        "metric": METRIC,
+        "value": round(2.0 * flops_total / (ms_step * 1e6), 3),
+        "unit": "GFLOP/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (deterministic band generator, ia-spgemm_amd/csrc/gen.cpp)",
+        "config": {"workload": desc + " (DIA format)", "kind": kind, **prm, "rows": rows,
+                   "diagonals_a": nda, "diagonals_c": ndc[0], "flops": flops_total, "format": "dia",
+                   "parallelism": "single GPU"},
+        "roofline": {
+            "kernel": "k_dia_mfma" if mfma else "k_dia_tile",
+            "bound": "hbm", "achieved": round(alg / (ms_k * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(alg / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+            "alg_bytes_per_launch": alg,
+            "alg_bytes_formula": "8*rows*(nd_A + nd_B + nd_C) + 4*(nd_A + nd_B + nd_C)",
+            "ms_per_launch": round(ms_k, 4),
+        },
+        "setup_s": round(t_gen, 2),
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
+    ias.lib.ias_dia_free(C.byref(da))
+    ias.lib.ias_plan_destroy(plan)
+    line = json.dumps(out)
+    print(line, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(line + "\n")
 
 
 def measure_allgatherv(step, c_rp, c_ci, c_va, reps=1):

@@ -53,6 +53,155 @@ __global__ __launch_bounds__(256) void k_dia_mul(int64_t rows, int64_t a_cols, i
     vc[e] = acc;
 }
 
+// LDS-tiled form: one workgroup per tile of TR consecutive rows.  The tile's A
+// rows (TR x nda) and the B rows they reach (TR + span(offa) rows x ndb) are
+// two contiguous ranges of the row-major DIA arrays: staged in LDS with
+// coalesced loads, so every A / B value is read from HBM once per tile (the
+// per-element kernel above re-reads them from L2 for each of the nd_C lanes
+// of a row).  The C tile (TR x nd_C) is one contiguous range: lanes over its
+// elements, non-temporal stores.  32-bit indexing inside the tile; e / nd_C
+// by a multiply-high.  Same per-element pair order as k_dia_mul (bitwise).
+struct DiaTileArgs {
+    int32_t rows, a_cols, b_cols;
+    int32_t nda, ndb, ndc, np;
+    int32_t lo_a, span_a;       // min A offset, max - min
+    int32_t tr;                 // rows per tile
+    uint64_t ndc_magic;         // ceil(2^32 / ndc)
+    const int32_t *offa, *offb;
+    const double *va, *vb;
+    const int32_t *tab;         // start[ndc + 1], ja[np], kb[np]
+    double *vc;
+};
+
+__global__ __launch_bounds__(256) void k_dia_tile(DiaTileArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int r0 = (int)blockIdx.x * a.tr;
+    const int tr = min(a.tr, a.rows - r0);
+    const int b0 = max(r0 + a.lo_a, 0);
+    const int b1 = min(r0 + tr - 1 + a.lo_a + a.span_a, a.a_cols - 1);   // inclusive
+    const int nbr = max(b1 - b0 + 1, 0);
+    double *sA = (double *)smem;
+    double *sB = sA + a.tr * a.nda;
+    int32_t *soa = (int32_t *)(sB + (a.tr + a.span_a) * a.ndb);
+    int32_t *sob = soa + a.nda;
+    int32_t *st = sob + a.ndb;
+    const int t = (int)threadIdx.x;
+    {
+        const double *ga = a.va + (int64_t)r0 * a.nda;
+        for (int i = t; i < tr * a.nda; i += 256) sA[i] = __builtin_nontemporal_load(ga + i);
+        const double *gb = a.vb + (int64_t)b0 * a.ndb;
+        for (int i = t; i < nbr * a.ndb; i += 256) sB[i] = gb[i];
+        for (int i = t; i < a.nda; i += 256) soa[i] = a.offa[i];
+        for (int i = t; i < a.ndb; i += 256) sob[i] = a.offb[i];
+        for (int i = t; i < a.ndc + 1 + 2 * a.np; i += 256) st[i] = a.tab[i];
+    }
+    __syncthreads();
+    const int32_t *sja = st + a.ndc + 1, *skb = sja + a.np;
+    const int n = tr * a.ndc;
+    double *gc = a.vc + (int64_t)r0 * a.ndc;
+    for (int e = t; e < n; e += 256) {
+        const int i = (int)(((uint64_t)(uint32_t)e * a.ndc_magic) >> 32);   // e / ndc (e < 2^20)
+        const int slot = e - i * a.ndc;
+        const int gi = r0 + i;
+        double acc = 0.0;
+        for (int p = st[slot]; p < st[slot + 1]; ++p) {
+            const int ja = sja[p], kb = skb[p];
+            const int acol = gi + soa[ja];
+            if (acol < 0 || acol >= a.a_cols) continue;
+            const int bcol = acol + sob[kb];
+            if (bcol < 0 || bcol >= a.b_cols) continue;
+            acc = acc + sA[i * a.nda + ja] * sB[(acol - b0) * a.ndb + kb];
+        }
+        __builtin_nontemporal_store(acc, gc + e);
+    }
+}
+
+// MFMA form (IAS_DIA_MFMA=1, A/B against k_dia_tile): the band of a tile of
+// 16 rows as dense blocks — A_t (16 x W_A, W_A = 16 + span(offa) columns from
+// i0 + min offa) times B_t (W_A x W_C, W_C = W_A + span(offb)) with
+// v_mfma_f64_16x16x4f64, operands built on the fly from the staged DIA rows
+// through offset -> diagonal maps (zeros off the band); the C block's band
+// elements go to their C diagonals.  The MFMA sums in its own order (fused,
+// not the reference's (0.0 + a*b) + a*b sequence), so this form matches the
+// reference within the north-star tolerance, not bitwise.  Waves of the
+// workgroup take the 16-column C blocks round-robin; C is zeroed first (the
+// DIA layout's off-matrix slots).
+typedef double dia_f64x4 __attribute__((ext_vector_type(4)));
+struct DiaMfmaArgs {
+    int32_t rows, a_cols, b_cols;
+    int32_t nda, ndb, ndc;
+    int32_t lo_a, span_a, lo_b, span_b, lo_c, span_c;
+    const int32_t *amap, *bmap, *cmap;   // offset - lo -> diagonal slot or -1
+    const double *va, *vb;
+    double *vc;
+};
+
+__global__ __launch_bounds__(256) void k_dia_mfma(DiaMfmaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int i0 = (int)blockIdx.x * 16;
+    const int WA = 16 + a.span_a, WC = WA + a.span_b;
+    const int cA0 = i0 + a.lo_a;           // global column of A_t column 0 (= B row of B_t row 0)
+    const int cC0 = cA0 + a.lo_b;          // global column of C_t column 0
+    double *sA = (double *)smem;                         // 16 x nda
+    double *sB = sA + 16 * a.nda;                        // WA x ndb (B rows cA0 ..)
+    int32_t *am = (int32_t *)(sB + WA * a.ndb);
+    int32_t *bm = am + a.span_a + 1;
+    int32_t *cm = bm + a.span_b + 1;
+    const int t = (int)threadIdx.x;
+    for (int i = t; i < 16 * a.nda; i += 256) {
+        const int r = i / a.nda;
+        sA[i] = i0 + r < a.rows ? a.va[(int64_t)(i0 + r) * a.nda + (i - r * a.nda)] : 0.0;
+    }
+    for (int i = t; i < WA * a.ndb; i += 256) {
+        const int r = i / a.ndb, br = cA0 + r;
+        sB[i] = (br >= 0 && br < a.a_cols) ? a.vb[(int64_t)br * a.ndb + (i - r * a.ndb)] : 0.0;
+    }
+    for (int i = t; i <= a.span_a; i += 256) am[i] = a.amap[i];
+    for (int i = t; i <= a.span_b; i += 256) bm[i] = a.bmap[i];
+    for (int i = t; i <= a.span_c; i += 256) cm[i] = a.cmap[i];
+    __syncthreads();
+    const int w = t >> 6, l = t & 63;
+    const int nblk = (WC + 15) / 16;
+    for (int cb = w; cb < nblk; cb += 4) {
+        dia_f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+        // A_t columns that reach this C block: c'' - c' in [0, span_b]
+        const int k_lo = max(0, cb * 16 - a.span_b), k_hi = min(WA, cb * 16 + 16);
+        for (int k0 = k_lo & ~3; k0 < k_hi; k0 += 4) {
+            const int kk = l >> 4, rr = l & 15;
+            const int ca = k0 + kk;                          // A_t column / B_t row
+            // A operand: A_t[rr][ca]; diagonal offset (cA0 + ca) - (i0 + rr)
+            const int oa = ca - rr;                          // minus lo_a
+            double av = 0.0;
+            if (oa >= 0 && oa <= a.span_a && ca < WA) {
+                const int ja = am[oa];
+                const int acol = cA0 + ca;
+                if (ja >= 0 && acol >= 0 && acol < a.a_cols) av = sA[rr * a.nda + ja];
+            }
+            // B operand: B_t[ca][cc], global column cC0 + cb*16 + cc
+            const int cc = l & 15;
+            const int ob = cb * 16 + cc - ca;                // (col - brow) - lo_b
+            double bv = 0.0;
+            if (ob >= 0 && ob <= a.span_b && ca < WA) {
+                const int kb = bm[ob];
+                const int col = cC0 + cb * 16 + cc;
+                if (kb >= 0 && col >= 0 && col < a.b_cols) bv = sB[ca * a.ndb + kb];
+            }
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        }
+        // C_t[row][col]: row = (l >> 4) + 4j, col = l & 15
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = (l >> 4) + 4 * j, col = l & 15;
+            const int gi = i0 + row, gc = cC0 + cb * 16 + col;
+            const int oc = (gc - gi) - a.lo_c;
+            if (gi < a.rows && cb * 16 + col < WC && gc >= 0 && gc < a.b_cols && oc >= 0 && oc <= a.span_c) {
+                const int d = cm[oc];
+                if (d >= 0) a.vc[(int64_t)gi * a.ndc + d] = acc[j];
+            }
+        }
+    }
+}
+
 __global__ void k_dia_index(int32_t ndc, const int32_t *offc, int64_t rows, int32_t *ind) {
     const int32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < ndc) ind[offc[d] + rows - 1] = d;
@@ -217,15 +366,61 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     HIPC(hipEventCreate(&e1));
     HIPC(hipEventRecord(e0, s));
     const int64_t n = A->rows * (int64_t)ndc;
+    const int32_t nda = A->num_diagonals, ndb = B->num_diagonals, np = (int32_t)pja.size();
     if (ndc > 0) {
         dev::k_dia_index<<<(ndc + 255) / 256, 256, 0, s>>>(ndc, D.diagonal_offsets, A->rows, D.diagonal_ind);
         if (n > 0) {
             const int32_t *t = (const int32_t *)dtab;
-            dev::DiaPairs pr{t, t + pst.size(), t + pst.size() + pja.size()};
-            dev::k_dia_mul<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
-                A->rows, A->cols, B->cols, A->num_diagonals, (const int32_t *)da_off,
-                (const double *)da_val, B->num_diagonals, (const int32_t *)db_off,
-                (const double *)db_val, ndc, pr, D.val);
+            const int32_t lo_a = *std::min_element(offa.begin(), offa.end());
+            const int32_t span_a = *std::max_element(offa.begin(), offa.end()) - lo_a;
+            const int32_t lo_b = *std::min_element(offb.begin(), offb.end());
+            const int32_t span_b = *std::max_element(offb.begin(), offb.end()) - lo_b;
+            const bool small = A->rows < (1ll << 30) && A->cols < (1ll << 30) && B->cols < (1ll << 30);
+            const char *mf = getenv("IAS_DIA_MFMA");
+            int32_t tr = 64;
+            auto tile_lds = [&](int32_t r) {
+                return 8ull * ((uint64_t)r * nda + (uint64_t)(r + span_a) * ndb) + 4ull * (nda + ndb + ndc + 1 + 2 * np);
+            };
+            while (tile_lds(tr) > 65536 && tr > 16) tr /= 2;
+            // MFMA for wide bands (measured: 65 diagonals, K1w, 0.57 ms vs 5.5 ms
+            // for the tiled VALU kernel; 7 diagonals, K1, 54 vs 32 us), VALU
+            // (bitwise the reference) otherwise; IAS_DIA_MFMA=0/1 forces either
+            const bool use_mfma = mf ? *mf == '1' : (int64_t)nda * ndb >= 256;
+            if (use_mfma && small) {
+                // offset -> slot maps for the dense-block operands
+                const int32_t lo_c = offc.front(), span_c = offc.back() - lo_c;
+                std::vector<int32_t> maps((size_t)span_a + span_b + span_c + 3, -1);
+                for (int32_t j = 0; j < nda; ++j) maps[offa[j] - lo_a] = j;
+                for (int32_t j = 0; j < ndb; ++j) maps[(size_t)span_a + 1 + (offb[j] - lo_b)] = j;
+                for (int32_t j = 0; j < ndc; ++j) maps[(size_t)span_a + span_b + 2 + (offc[j] - lo_c)] = j;
+                const void *dmaps;
+                IAS_TRY(stage(maps.data(), 4 * maps.size(), IAS_MEMORY_HOST, 0, &dmaps));
+                const int32_t *m = (const int32_t *)dmaps;
+                const int32_t WA = 16 + span_a;
+                const size_t lds = 8ull * (16ull * nda + (uint64_t)WA * ndb) + 4ull * maps.size();
+                if (lds > 160 * 1024) return IAS_ERROR_INVALID_ARGUMENT;
+                if (lds > 65536)
+                    hipFuncSetAttribute((const void *)dev::k_dia_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024);
+                HIPC(hipMemsetAsync(D.val, 0, 8 * (size_t)n, s));
+                dev::DiaMfmaArgs ma{(int32_t)A->rows, (int32_t)A->cols, (int32_t)B->cols, nda, ndb, ndc,
+                                    lo_a, span_a, lo_b, span_b, lo_c, span_c,
+                                    m, m + span_a + 1, m + span_a + span_b + 2,
+                                    (const double *)da_val, (const double *)db_val, D.val};
+                dev::k_dia_mfma<<<(unsigned)((A->rows + 15) / 16), 256, lds, s>>>(ma);
+            } else if (small && tile_lds(tr) <= 65536) {
+                const uint64_t magic = ((1ull << 32) + (uint64_t)ndc - 1) / (uint64_t)ndc;
+                dev::DiaTileArgs ta{(int32_t)A->rows, (int32_t)A->cols, (int32_t)B->cols, nda, ndb, ndc, np,
+                                    lo_a, span_a, tr, magic, (const int32_t *)da_off, (const int32_t *)db_off,
+                                    (const double *)da_val, (const double *)db_val, t, D.val};
+                dev::k_dia_tile<<<(unsigned)((A->rows + tr - 1) / tr), 256, tile_lds(tr), s>>>(ta);
+            } else {
+                dev::DiaPairs pr{t, t + pst.size(), t + pst.size() + pja.size()};
+                dev::k_dia_mul<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
+                    A->rows, A->cols, B->cols, A->num_diagonals, (const int32_t *)da_off,
+                    (const double *)da_val, B->num_diagonals, (const int32_t *)db_off,
+                    (const double *)db_val, ndc, pr, D.val);
+            }
         }
     }
     HIPC(hipGetLastError());

@@ -168,6 +168,8 @@ ias_status ias_plan_destroy(ias_plan *plan);
 ias_status ias_csr_alloc(ias_csr *m, int64_t rows, int64_t cols, int64_t nnz,
                          int32_t memory, int32_t device);
 ias_status ias_csr_copy(const ias_csr *src, ias_csr *dst, int32_t memory, int32_t device);
+/* Device arrays go back to a per-device block cache (reused by later calls
+ * on that device) instead of hipFree; finish your own work on them first. */
 ias_status ias_csr_free(ias_csr *m);   /* FreeCsrMatrix  csr/common_csr.h:307-317 */
 ias_status ias_coo_free(ias_coo *m);   /* FreeCooMatrix  coo/common_coo.h:185-195 */
 ias_status ias_ell_free(ias_ell *m);   /* FreeEllMatrix  ell/common_ell.h:232-244 */
@@ -226,6 +228,10 @@ ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_coo *C,
                            const ias_opts *opts, ias_report *report);  /* COO_MUL_COO coo:72-161 */
 ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_ell *C,
                            const ias_opts *opts, ias_report *report);  /* ELL_MUL_ELL ell:80-189 */
+/* DIA: bitwise the reference for narrow bands (LDS-tiled VALU kernel); bands
+ * with nd_A * nd_B >= 256 use f64 MFMA dense blocks (fused sums: within the
+ * north-star 1e-10 relative tolerance, not bitwise); IAS_DIA_MFMA=0/1 in the
+ * environment forces either kernel. */
 ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
                            const ias_opts *opts, ias_report *report);  /* DIA_mul_DIA dia:101-195 */
 

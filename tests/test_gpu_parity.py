@@ -326,29 +326,71 @@ def test_ell_synthetic(case):
     np.testing.assert_array_equal(bits(got_v), bits(ref["val"]))
 
 
+def _sparse_band(n=3000, seed=4):
+    """Non-contiguous diagonal set (offsets -40, -7, 0, 3, 11, 90) with a few
+    holes on each diagonal: the offset -> slot maps have gaps."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for i in range(n):
+        cols = [i + o for o in (-40, -7, 0, 3, 11, 90) if 0 <= i + o < n and rng.random() > 0.05]
+        rows.append(np.array(sorted(cols), np.int64))
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    return ias.HostCsr(n, n, rp, col, rng.standard_normal(col.size))
+
+
 DIA_CASES = [("band4k", lambda: ias.gen_band(4096, 3, seed=7)),
              ("band_w1", lambda: ias.gen_band(1000, 1, seed=3, value_mode=1)),
+             ("band_wide65", lambda: ias.gen_band(5000, 32, seed=5)),
+             ("band_sparse_offsets", _sparse_band),
              ("dia.mtx", None), ("small.mtx", None), ("b1_ss.mtx", None)]
 
 
-@pytest.mark.parametrize("case", DIA_CASES, ids=lambda c: c[0])
-def test_dia(case, inputs_dir):
-    name, mk = case
-    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
-    ref = ob.dia_mul_dia(ob.Mat.of(A), ob.Mat.of(A))
+def _dia_run(A, mfma, monkeypatch):
+    monkeypatch.setenv("IAS_DIA_MFMA", "1" if mfma else "0")
     s = A.struct()
     da, dc = ias.Dia(), ias.Dia()
     ias.check(ias.lib.ias_csr_to_dia(C.byref(s), C.byref(da), 0.0), "to_dia")
     o = ias.opts(output_memory=ias.MEMORY_HOST)
     ias.check(ias.lib.ias_dia_mul_dia(C.byref(da), C.byref(da), C.byref(dc), C.byref(o), None), "dia")
     nd = dc.num_diagonals
-    assert nd == ref["nd"]
-    np.testing.assert_array_equal(ias._np(dc.diagonal_offsets, nd, np.int32), ref["offsets"])
-    np.testing.assert_array_equal(ias._np(dc.diagonal_ind, dc.rows + dc.cols - 1, np.int32), ref["ind"])
-    got_v = ias._np(dc.val, dc.rows * nd, np.float64).reshape(dc.rows, nd)
-    np.testing.assert_array_equal(bits(got_v), bits(ref["val"]))
+    out = dict(nd=nd, offsets=ias._np(dc.diagonal_offsets, nd, np.int32).copy(),
+               ind=ias._np(dc.diagonal_ind, dc.rows + dc.cols - 1, np.int32).copy(),
+               val=ias._np(dc.val, dc.rows * nd, np.float64).reshape(dc.rows, nd).copy())
     ias.lib.ias_dia_free(C.byref(da))
     ias.lib.ias_dia_free(C.byref(dc))
+    return out
+
+
+@pytest.mark.parametrize("case", DIA_CASES, ids=lambda c: c[0])
+def test_dia(case, inputs_dir, monkeypatch):
+    """The LDS-tiled kernel (default): bitwise the reference's DIA_mul_DIA."""
+    name, mk = case
+    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
+    ref = ob.dia_mul_dia(ob.Mat.of(A), ob.Mat.of(A))
+    got = _dia_run(A, False, monkeypatch)
+    assert got["nd"] == ref["nd"]
+    np.testing.assert_array_equal(got["offsets"], ref["offsets"])
+    np.testing.assert_array_equal(got["ind"], ref["ind"])
+    np.testing.assert_array_equal(bits(got["val"]), bits(ref["val"]))
+
+
+@pytest.mark.parametrize("case", DIA_CASES, ids=lambda c: c[0])
+def test_dia_mfma(case, inputs_dir, monkeypatch):
+    """The MFMA form (IAS_DIA_MFMA=1, fused sums in the matrix core's order):
+    same diagonal set, values within the north-star tolerance
+    |dC| <= 1e-10 * max(|c|, sum |a*b|)."""
+    name, mk = case
+    A = mk() if mk else ias.mtx_read(os.path.join(inputs_dir, name))[0]
+    ref = ob.dia_mul_dia(ob.Mat.of(A), ob.Mat.of(A))
+    absA = ias.HostCsr(A.rows, A.cols, A.row_ptr, A.col, np.abs(A.val))
+    bound = ob.dia_mul_dia(ob.Mat.of(absA), ob.Mat.of(absA))["val"]
+    got = _dia_run(A, True, monkeypatch)
+    assert got["nd"] == ref["nd"]
+    np.testing.assert_array_equal(got["offsets"], ref["offsets"])
+    tol = 1e-10 * np.maximum(np.abs(ref["val"]), bound) + 1e-300
+    assert np.all(np.abs(got["val"] - ref["val"]) <= tol)
 
 
 # ------------------------------------------------------------------ device-side conversions (f3)
