@@ -1791,14 +1791,14 @@ ias_status ias_plan::init(int dev, void *strm) {
 }
 
 ias_status ias_plan::fork() {
-    if (serial) return IAS_SUCCESS;
+    if (serial || small) return IAS_SUCCESS;
     HIPC(hipEventRecord(fork_ev, (hipStream_t)stream));
     for (int i = 0; i < NSIDE; ++i) HIPC(hipStreamWaitEvent((hipStream_t)side[i], fork_ev, 0));
     return IAS_SUCCESS;
 }
 
 ias_status ias_plan::join() {
-    if (serial) return IAS_SUCCESS;
+    if (serial || small) return IAS_SUCCESS;
     for (int i = 0; i < NSIDE; ++i) {
         HIPC(hipEventRecord(join_ev[i], (hipStream_t)side[i]));
         HIPC(hipStreamWaitEvent((hipStream_t)stream, join_ev[i], 0));
@@ -1899,6 +1899,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         return IAS_ERROR_INVALID_ARGUMENT;
     }
     flops = (int64_t)c1.flops;
+    small = flops < SMALL_FLOPS;
     max_prod = c1.max_prod;
 
     // ---- expansion: every row's product columns, contiguous (sym2: only the

@@ -85,7 +85,12 @@ struct ias_plan {
     ias_status fork();
     ias_status join();
     bool serial = false;   // IAS_SERIAL=1: everything on `stream` (per-kernel profiling)
-    void *side_stream(int i) const { return serial ? stream : side[i % NSIDE]; }
+    // small products (flops < SMALL_FLOPS): the bins run on `stream` too — a
+    // fork / join across queues costs ~30 us of event latency each, more than
+    // the bins of a small product overlap
+    bool small = false;
+    static constexpr int64_t SMALL_FLOPS = 64ll << 20;
+    void *side_stream(int i) const { return (serial || small) ? stream : side[i % NSIDE]; }
     void *host_counters = nullptr;
 
     // state carried from symbolic() to numeric()
