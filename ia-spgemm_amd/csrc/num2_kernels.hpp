@@ -81,7 +81,11 @@ __device__ __forceinline__ void st16(void *p, uint4 v) {
 #define N2_K 4
 #endif
 
-__global__ __launch_bounds__(64 * N2_WPB) void k_num2(Num2Args a, Out out) {
+#ifndef N2_WPE
+#define N2_WPE 1   // minimum waves per SIMD the register allocation must allow (1: no cap)
+#endif
+__global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_WPE))) void k_num2(Num2Args a,
+                                                                                                 Out out) {
     constexpr int K = N2_K;
     constexpr int PASS = 64 * K;   // staged C entries per step (at most one per product)
     struct Ent {

@@ -198,6 +198,9 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    Timer tm;   // timing builds only (phases: 0 wait for row i's columns, 1 stage row i+1, 2 gather
+                // row i+1 + prefetch issue, 7 filter pass 3a, 4 classify 3b, 3 exact, 5 finish,
+                // 6 final barrier)
     // f1, f2 zero and the exact table empty, for the next row
     auto clear_tables = [&]() __attribute__((always_inline)) {
         for (uint32_t i = lane; i < L.FW / 2; i += TEAM) ((uint4 *)f1)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -298,6 +301,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             }
         }
         TM::sync();
+        tm.mark(7);
         // 3b. classify: certain first touches -> bitmap words; possible
         // duplicates -> list (one list atomic per wave and chunk)
 #pragma unroll
@@ -344,6 +348,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             }
         }
         TM::sync();
+        tm.mark(4);
         const int32_t nl = *lcount;
         if ((uint32_t)nl > L.LC) {
             // heavy row: count distinct columns in a keys-only table over f1 .. own
@@ -368,7 +373,37 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             if (lane == 0) *hcount = tot;
             return -1;
         }
-        if (nl > 0) {
+        if (TM::MULTI && nl > 0 && nl <= WAVE) {
+            // 4'. a short list (the common case: a few % of the products): the
+            // team's first wave resolves it alone with wave-level syncs, one
+            // team barrier instead of three
+            if (lane < WAVE) {
+                uint32_t s = 0;
+                bool won = false;
+                int2 e = make_int2(0, 0);
+                if (lane < nl) {
+                    e = list[lane];
+                    s = reduce32(fib(e.x), L.ES);
+                    for (uint32_t probe = 0; probe < L.ES; ++probe) {
+                        const int32_t g = atomicCAS(&keys[s], EMPTY_KEY, e.x);
+                        if (g == EMPTY_KEY) { won = true; break; }
+                        if (g == e.x) break;
+                        s = (s + 1u == L.ES) ? 0u : s + 1u;
+                    }
+                    if (won) own[s] = (uint32_t)e.y;
+                }
+                wave_sync();
+                if (lane < nl && !won) atomicMin(&own[s], (uint32_t)e.y);
+                wave_sync();
+                if (lane < nl) {
+                    const uint32_t p = (uint32_t)e.y;
+                    const uint32_t f = own[s];
+                    if (f == p) atomicOr(&lbits[p >> 5], 1u << (p & 31));
+                    list[lane] = make_int2((int32_t)p, (int32_t)f);
+                }
+            }
+            TM::sync();
+        } else if (nl > 0) {
             // 4. exact: claim a slot per column (linear probing), winners own it
             for (int32_t i = lane; i < nl; i += TEAM) {
                 const int2 e = list[i];
@@ -459,8 +494,6 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     }
     Sym2Row nxt = sym2_detail<TEAM>(a, sym2_ref<TEAM>(a, idx + nteams));
     RowRef nref = sym2_ref<TEAM>(a, idx + 2 * nteams);
-    Timer tm;   // timing builds only (phases: 0 wait for row i's columns, 1 stage row i+1, 2 gather
-                // row i+1 + prefetch issue, 3 filter + exact, 5 finish, 6 final barrier)
     tm.start();
     // Software pipeline, per iteration (row i): stage + gather row i+1, its
     // column loads then fly during row i's resolution; prefetch row i+2's
