@@ -198,7 +198,7 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
             av[u] = 0.0;
             if (ok[u]) {
                 B.row(j[u], bs[u], bn[u]);
-                av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
+                if (ax.aval) av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
             }
         }
 #pragma unroll
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
             if (q >= a_entries) continue;
             ax.bstart[q] = bs[u];
             ax.blen[q] = bn[u];
-            ax.aval[q] = av[u];
+            if (ax.aval) ax.aval[q] = av[u];
             if (!A.ptr) ax.row[q] = (int32_t)(q / A.stride);
         }
     }
@@ -867,7 +867,8 @@ __global__ __launch_bounds__(1024) void k_fixup_big(const RowRef *list, int32_t 
 // Row-wise analysis helpers: product offset of every row, and the expansion
 // of every A entry's products into tcol (one wave per FLAT_CHUNK entries,
 // lanes over the chunk's products: coalesced B-row reads, contiguous writes).
-__global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_entries, int64_t *poff) {
+__global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_entries, int64_t *poff,
+                           Counters *cnt) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r > rows) return;
     if (r == rows) {
@@ -877,7 +878,12 @@ __global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_e
     int64_t s;
     int32_t n;
     A.row(r, s, n);
-    poff[r] = axp[s - A.base()];
+    int64_t q = s - A.base();
+    if (q < 0 || n < 0 || q + n > n_entries) {   // row pointer disagrees with the declared entry count
+        cnt->overflow = 1;
+        q = q < 0 ? 0 : (q > n_entries ? n_entries : q);
+    }
+    poff[r] = axp[q];
 }
 
 // Product -> entry mapping without a per-product search: the wave's chunk of
@@ -1785,7 +1791,7 @@ ias_status ias_plan::init(int dev, void *strm) {
     HIPC(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     const char *e = getenv("IAS_SERIAL");
     serial = e && *e && *e != '0';
-    HIPC(hipHostMalloc(&host_counters, 2 * sizeof(Counters)));
+    HIPC(hipHostMalloc(&host_counters, 3 * sizeof(Counters)));   // [0], [1]: counters; [2]: A's base
     HIPC(hipHostMalloc(&host_info, 64));
     return IAS_SUCCESS;
 }
@@ -1809,13 +1815,17 @@ ias_status ias_plan::join() {
 template <typename T>
 static T *as(ias_plan::Buf &b) { return (T *)b.p; }
 
+// The A value of expanded entry q is A.val[base + q] (CSR: base = the view's
+// first row pointer, read back with the analysis counters; ELL: 0), so the
+// expanded A carries no copy of the values.
 AxView ias_plan::ax_view() {
-    return AxView{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), as<double>(bufs[B_AXV])};
+    return AxView{as<int64_t>(bufs[B_AXS]), as<int32_t>(bufs[B_AXL]), ax_aval};
 }
 
 // Analysis (queued, no host wait): products per row, expanded A, product
 // offsets per entry and per row, symbolic bin counts into the B_CNT counters.
-ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries) {
+ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries,
+                                     bool need_rows) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
@@ -1824,7 +1834,6 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
-    IAS_TRY(reserve(B_AXV, sizeof(double) * ae));
     IAS_TRY(reserve(B_AXR, sizeof(int32_t) * ae));
     IAS_TRY(reserve(B_AXP, sizeof(int64_t) * (ae + 1)));
     IAS_TRY(reserve(B_POFF, sizeof(int64_t) * (rows + 1)));
@@ -1854,13 +1863,15 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     int32_t *axr = as<int32_t>(bufs[B_AXR]);
     int64_t *axp = as<int64_t>(bufs[B_AXP]);
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
-    if (A.ptr && rows > 0)
+    // the row of every A entry: only the flat numeric pass (IAS_NUM2=0) and the
+    // single-pass engine read it (k_row_poff validates the row pointer)
+    if (A.ptr && rows > 0 && need_rows)
         k_an_rowfill<<<grid_for(rows * AN_FILL, 256), 256, 0, s>>>(A, rows, a_entries, axr, dc);
     if (a_entries > 0) {
         const int64_t per = (int64_t)AN_BLOCK * AN_U;
         const unsigned g = (unsigned)std::min<int64_t>((a_entries + per - 1) / per, 16384);
         k_an_entries<<<g, AN_BLOCK, 0, s>>>(A, B, a_entries,
-                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, as<double>(bufs[B_AXV]), axr});
+                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, axr});
     }
     CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
@@ -1870,7 +1881,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     } else {
         HIPC(hipMemsetAsync(axp, 0, sizeof(int64_t), s));
     }
-    k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff);
+    k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff, dc);
     if (rows > 0)
         k_an_rows<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
     CHECK_LAUNCH("product offsets", s);
@@ -1881,19 +1892,23 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
 ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
                               int64_t a_entries, ias_report *rep) {
     (void)cols;
-    IAS_TRY(analysis_launch(A, B, rows, a_entries));
+    IAS_TRY(analysis_launch(A, B, rows, a_entries, !num2_on()));
     hipStream_t s = (hipStream_t)stream;
     const BinSpec ss = sym_spec(), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT2]);
     Counters *hc = (Counters *)host_counters;
-    const AxView ax = ax_view();
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
     const int64_t *axp = as<int64_t>(bufs[B_AXP]);
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    int64_t *a_base = (int64_t *)(hc + 2);
+    *a_base = 0;
+    if (A.ptr) HIPC(hipMemcpyAsync(a_base, A.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
+    ax_aval = A.val + *a_base;
+    const AxView ax = ax_view();
     if (c1.overflow) {
         set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
         return IAS_ERROR_INVALID_ARGUMENT;
@@ -2194,7 +2209,7 @@ ias_status ias_plan::onepass_prepare(const Rows &A, const Rows &B, int64_t rows,
                                      int64_t a_entries, ias_report *rep) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
-    IAS_TRY(analysis_launch(A, B, rows, a_entries));
+    IAS_TRY(analysis_launch(A, B, rows, a_entries, true));
     const size_t rn = (size_t)rows + 2;
     IAS_TRY(reserve(B_OPCF, sizeof(int32_t) * rn));
     IAS_TRY(reserve(B_OPBF, sizeof(int32_t) * rn));
@@ -2232,8 +2247,12 @@ ias_status ias_plan::onepass_prepare(const Rows &A, const Rows &B, int64_t rows,
     }
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+    int64_t *a_base = (int64_t *)(hc + 2);
+    *a_base = 0;
+    if (A.ptr) HIPC(hipMemcpyAsync(a_base, A.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
+    ax_aval = A.val + *a_base;
     if (c1.overflow) {
         set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
         return IAS_ERROR_INVALID_ARGUMENT;

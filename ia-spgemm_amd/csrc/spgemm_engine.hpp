@@ -114,7 +114,8 @@ struct ias_plan {
     ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
     // a_entries: stored entries of A (CSR: nnz of the view; ELL: rows * width)
     ias_status analysis_launch(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
-                               int64_t a_entries);
+                               int64_t a_entries, bool need_rows);
+    const double *ax_aval = nullptr;   // A.val + the view's base (set after the analysis read-back)
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                         int64_t cols, int64_t a_entries, ias_report *rep);
     ias::dev::AxView ax_view();
