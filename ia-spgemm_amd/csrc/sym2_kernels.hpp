@@ -350,8 +350,9 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         TM::sync();
         tm.mark(4);
         const int32_t nl = *lcount;
-        if ((uint32_t)nl > L.LC) {
+        if ((uint32_t)nl > L.LC || (a.ablate & 4)) {
             // heavy row: count distinct columns in a keys-only table over f1 .. own
+            // (IAS_S2_ABLATE & 4: every row, an A/B of table-path numeric)
             int32_t *hk = (int32_t *)f1;
             const uint32_t HS = L.heavy_slots();
             for (uint32_t i = lane; i < HS; i += TEAM) hk[i] = EMPTY_KEY;
