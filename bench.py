@@ -513,6 +513,16 @@ def measure_allgatherv(step, c_rp, c_ci, c_va, reps=1):
         step()
         return gather_csr(c_rp, c_ci, c_va, mode="all")
 
+    # the gathered C must fit next to everything this rank holds
+    tot = torch.tensor([int(c_ci.numel()), int(c_rp.numel()) - 1], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot)
+    need = 12 * int(tot[0]) + 8 * (int(tot[1]) + 1)
+    if dev.type == "cuda":
+        free = torch.tensor([torch.cuda.mem_get_info(dev)[0]], dtype=torch.int64, device=dev)
+        dist.all_reduce(free, op=dist.ReduceOp.MIN)
+        if need > 0.8 * int(free.item()):
+            return {"what": "skipped: the gathered C would not fit", "c_bytes": need,
+                    "free_bytes_min": int(free.item())}
     mc, mcg = [], []
     full_nnz = full_rows = 0
     for _ in range(max(1, reps)):
