@@ -1346,6 +1346,9 @@ constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
 // lane, 4 teams per workgroup: no workgroup barrier per row), 4..7 = 128- to
 // 1024-lane teams with K = 8 (one-wave teams with K = 16 / 32 measured slower:
 // 160-256 VGPRs, 2-3 waves per SIMD).
+#ifndef SYM2_CFG7_ALT
+#define SYM2_CFG7_ALT 0
+#endif
 #ifndef SYM2_WIDE
 #define SYM2_WIDE 1   // rows of 8193..16384 products on sym2 (else the partitioned path)
 #endif
@@ -1625,6 +1628,7 @@ static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, u
 
 static Sym2Layout sym2_layout(int32_t upper, int cfg) {
     // 8 filter bits keep the widest bin's team within one CU's LDS
+    if (SYM2_CFG7_ALT && cfg == 7) return Sym2Layout::for_bound((uint32_t)upper, Sym2Layout::ONE_WAVE);
     return Sym2Layout::for_bound((uint32_t)upper, cfg == SYM2_CFG_WIDE     ? Sym2Layout::WIDE
                                                   : cfg <= SYM2_WAVE_CFG_MAX ? Sym2Layout::ONE_WAVE
                                                                              : Sym2Layout::TEAM_LAYOUT);
@@ -1653,7 +1657,11 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
         case 4: sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(a, s); break;   // one-wave K=16 measured 30 % slower
         case 5: sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(a, s); break;
         case 6: sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+#if SYM2_CFG7_ALT
+        case 7: sym2_launch<512, 16, 1, 4>(a, s); break;   // A/B: two teams per CU, compact layout
+#else
         case 7: sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(a, s); break;
+#endif
         default: sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(a, s); break;   // SYM2_CFG_WIDE
     }
 }
