@@ -284,6 +284,10 @@ def main(argv=None):
         kname = "k_onepass" if args.engine == "onepass" else \
             ("k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2")
         units = {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)}
+        # the pass is 1 or 2 launches (rows with duplicates first, their fix-ups
+        # then overlap the rest): per launch = the pass's bytes and time / launches,
+        # which is what rocprofv3's average launch duration of the kernel shows
+        launches = max(1, int(getattr(rep, "stream_launches", 1) or 1))
         if args.engine == "twophase" and int(rep.stream_nnz) < local_nnz // 2:
             # most of C comes from the short-row / table kernels (K1, K2): the
             # dominant unit is then the whole numeric phase (event-timed), its
@@ -293,6 +297,7 @@ def main(argv=None):
             flat_bytes = 12 * local_nnz + bytes_a + bytes_b
             gather_bytes = 12 * int(rep_s.flops)
             units = {"products": int(rep_s.flops), "c_entries": local_nnz}
+            launches = 1
         achieved = flat_bytes / (ms_flat * 1e-3) / 1e9 if ms_flat > 0 else 0.0
         traffic, lds_conf = None, None
         pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.config}_n{world_req}.json")
@@ -340,12 +345,14 @@ def main(argv=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
-                "alg_bytes_per_launch": flat_bytes,
+                "alg_bytes_per_launch": flat_bytes // launches,
+                "launches_per_pass": launches,
+                "ms_per_pass": round(ms_flat, 4),
                 "alg_bytes_formula": "12*c_entries + bytes(A) + bytes(B), bytes(X) = 8*(rows+1) + 12*nnz(X)",
                 "gather_bytes": gather_bytes,
                 "lds_bank_conflict_ratio": lds_conf,
-                "ms_per_launch": round(ms_flat, 4),
-                "units_per_launch": units,
+                "ms_per_launch": round(ms_flat / launches, 4),
+                "units_per_pass": units,
             },
             "roofline_step": {
                 "what": "whole step: B_alg = bytes(A) + bytes(B) + bytes(C) (SURVEY 8 d3) / step time",

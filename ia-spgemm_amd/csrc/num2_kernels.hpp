@@ -24,6 +24,7 @@
 #pragma once
 
 #include "spgemm_kernels.hpp"
+#include "spgemm_engine.hpp"   // Counters
 
 namespace ias {
 namespace dev {
@@ -50,21 +51,39 @@ struct Num2Args {
     double *dupval;
 };
 
-// Units: every streaming row with products gets ceil(entries / 64) of them.
+// Units: every streaming row with products gets ceil(entries / 64) of them,
+// counted in three lists — rows with more than N2_BIGDUP duplicates (the
+// sorted fix-ups of long lists), rows with fewer, rows without — at
+// cnt[cls*rows + r], so one scan over 3*rows orders the units by class: each
+// class's fix-ups can start once its units are done.
+constexpr int32_t N2_BIGDUP = 1024;   // = FIXMID_CAP
 __global__ void k_num2_count(Rows A, int64_t rows, const int32_t *dupn, const int32_t *prod, int32_t *cnt) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rows) return;
     int64_t s;
     int32_t n;
     A.row(r, s, n);
-    cnt[r] = (dupn[r] >= 0 && prod[r] > 0) ? (n + N2_ENT - 1) / N2_ENT : 0;
+    const int32_t d = dupn[r];
+    const int32_t u = (d >= 0 && prod[r] > 0) ? (n + N2_ENT - 1) / N2_ENT : 0;
+    const int cls = d > N2_BIGDUP ? 0 : (d > 0 ? 1 : 2);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) cnt[c * rows + r] = c == cls ? u : 0;
 }
-__global__ void k_num2_fill(int64_t rows, const int32_t *cnt, const int64_t *uoff, Num2Unit *units) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= rows) return;
-    const int32_t c = cnt[r];
-    const int64_t o = uoff[r];
-    for (int32_t i = 0; i < c; ++i) units[o + i] = Num2Unit{(int32_t)r, i * N2_ENT};
+// uoff: exclusive scan of cnt[0 .. 3*rows] (uoff[3*rows] = all units); thread 0
+// also stores the unit count and the class boundaries in the counters
+__global__ void k_num2_fill(int64_t rows, const int32_t *cnt, const int64_t *uoff, Num2Unit *units,
+                            Counters *tot) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        tot->n2_units = (unsigned long long)uoff[3 * rows];
+        tot->n2_bunits = (unsigned long long)uoff[rows];
+        tot->n2_dunits = (unsigned long long)uoff[2 * rows];
+    }
+    if (i >= 3 * rows) return;
+    const int32_t c = cnt[i];
+    const int64_t o = uoff[i];
+    const int32_t r = (int32_t)(i % rows);
+    for (int32_t j = 0; j < c; ++j) units[o + j] = Num2Unit{r, j * N2_ENT};
 }
 
 // 16-byte non-temporal store (C is not read back by this pass)

@@ -7,6 +7,7 @@
 #include "onepass_kernels.hpp"
 #include "sym2_kernels.hpp"
 #include "num2_kernels.hpp"
+#include <functional>
 #include "short_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
@@ -252,7 +253,10 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
     if (threadIdx.x == 0) {
         for (int i = 0; i < BIN_BLOCK / WAVE; ++i) mx = max(mx, wmx[i]);
         if (mx > 0) atomicMax(&cnt->max_prod, mx);
-        if (blockIdx.x == 0) cnt->flops = (unsigned long long)(poff[rows] - poff[0]);
+        if (blockIdx.x == 0) {
+            cnt->flops = (unsigned long long)(poff[rows] - poff[0]);
+            cnt->a_base = (long long)A.base();
+        }
     }
 }
 
@@ -261,7 +265,9 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
 // streaming-class when stn is given and stn[r] >= 0.
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, const int32_t *prod,
                                                          const int32_t *stn, int64_t rows,
-                                                         BinSpec spec, Counters *cnt) {
+                                                         BinSpec spec, Counters *cnt,
+                                                         const int64_t *total = nullptr) {
+    if (total && blockIdx.x == 0 && threadIdx.x == 0) cnt->nnz_total = (unsigned long long)*total;
     int b[BIN_RPT];
     int32_t k[BIN_RPT];
     unsigned long long sp = 0, sn = 0;
@@ -796,6 +802,7 @@ __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int
                                                         const int32_t *gdupt, const double *gdupval,
                                                         Out out) {
     __shared__ int32_t dupt[FIX_TPW][256];
+    __shared__ double dval[FIX_TPW][256];
     const int team = threadIdx.x / WAVE;
     const int64_t idx = (int64_t)blockIdx.x * FIX_TPW + team;
     if (idx >= count) return;
@@ -804,7 +811,7 @@ __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int
     if (nd <= 0 || nd > 256) return;
     const int64_t off = bm.off[row];
     numeric_fixup_row<WAVE>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
-                            gdupval + dup_off[row], nd, dupt[team], out);
+                            gdupval + dup_off[row], nd, dupt[team], dval[team], out);
 }
 
 // Duplicate fix-up of streaming rows with short lists (<= 16): one lane per
@@ -854,17 +861,48 @@ __global__ __launch_bounds__(256) void k_fixup_tiny(const RowRef *list, int32_t 
 #ifndef FIXBIG_CAP_DEF
 #define FIXBIG_CAP_DEF 8192   // 16384 (128 KB of LDS, one block per CU): K3 37.3 vs 36.0 ms
 #endif
-constexpr int FIXBIG_CAP = FIXBIG_CAP_DEF;   // keys in dynamic LDS: 8 B each (128 KB)
+constexpr int FIXBIG_CAP = FIXBIG_CAP_DEF;   // keys (then values) in dynamic LDS: 8 B each, + run-head bits
+constexpr size_t FIXBIG_LDS = 8ull * FIXBIG_CAP + FIXBIG_CAP / 8;
+// Lists of at most FIXMID_CAP: 256 lanes and 16 KB of LDS, so several rows per
+// CU (and room beside the streaming pass's waves); longer lists: k_fixup_large
+// / k_fixup_big.
+constexpr int FIXMID_CAP = 1024;
+__global__ __launch_bounds__(256) void k_fixup_mid(const RowRef *list, int32_t count, Bitmap bm,
+                                                  const int64_t *dup_off, const int32_t *dupn,
+                                                  const int32_t *gdupt, const double *gdupval, Out out) {
+    __shared__ unsigned long long key[2 * FIXMID_CAP + FIXMID_CAP / 64];
+    const int64_t row = list[blockIdx.x].row;
+    const int32_t nd = dupn[row];
+    if (nd <= 0 || nd > FIXMID_CAP) return;
+    const int64_t off = bm.off[row];
+    numeric_fixup_lds<256, FIXMID_CAP>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
+                                       gdupval + dup_off[row], nd, key, out);
+}
+// Lists of FIXMID_CAP+1 .. FIXLARGE_CAP: 256 lanes and 64 KB, small enough to
+// sit beside the streaming pass's waves on a CU.
+constexpr int FIXLARGE_CAP = 4096;
+constexpr size_t FIXLARGE_LDS = 8ull * (2 * FIXLARGE_CAP + FIXLARGE_CAP / 64);
+__global__ __launch_bounds__(256) void k_fixup_large(const RowRef *list, int32_t count, Bitmap bm,
+                                                    const int64_t *dup_off, const int32_t *dupn,
+                                                    const int32_t *gdupt, const double *gdupval, Out out) {
+    extern __shared__ unsigned long long key[];   // FIXLARGE_LDS bytes (dynamic: > 64 KB)
+    const int64_t row = list[blockIdx.x].row;
+    const int32_t nd = dupn[row];
+    if (nd <= FIXMID_CAP || nd > FIXLARGE_CAP) return;
+    const int64_t off = bm.off[row];
+    numeric_fixup_lds<256, FIXLARGE_CAP>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
+                                         gdupval + dup_off[row], nd, key, out);
+}
 __global__ __launch_bounds__(1024) void k_fixup_big(const RowRef *list, int32_t count, Bitmap bm,
                                                    const int64_t *dup_off, const int32_t *dupn,
                                                    const int32_t *gdupt, const double *gdupval, Out out) {
     extern __shared__ unsigned long long key[];
     const int64_t row = list[blockIdx.x].row;
     const int32_t nd = dupn[row];
-    if (nd <= 0 || nd > FIXBIG_CAP) return;
+    if (nd <= FIXLARGE_CAP || nd > FIXBIG_CAP) return;
     const int64_t off = bm.off[row];
-    numeric_fixup_big<1024>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row], gdupval + dup_off[row],
-                            nd, key, FIXBIG_CAP, out);
+    numeric_fixup_big<1024, FIXBIG_CAP>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
+                                        gdupval + dup_off[row], nd, key, out);
 }
 
 // Row-wise analysis helpers: product offset of every row, and the expansion
@@ -1379,6 +1417,18 @@ static bool num2_on() {
     }();
     return on;
 }
+// IAS_N2_SPLIT=0: one k_num2 launch, the fix-ups after it on its stream
+// (default: up to three launches — units of rows with > 1024 duplicates, with
+// fewer, without — the longest lists' 1024-lane fix-ups right after the first
+// launch on its stream, the other fix-ups of each class on another stream
+// alongside the later launches).
+static bool n2_split_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_N2_SPLIT");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
@@ -1777,6 +1827,8 @@ ias_plan::~ias_plan() {
         if (join_ev[i]) hipEventDestroy(join_ev[i]);
     }
     if (fork_ev) hipEventDestroy(fork_ev);
+    for (auto &e : fix_ev)
+        if (e) hipEventDestroy(e);
     if (host_counters) hipHostFree(host_counters);
     if (host_info) hipHostFree(host_info);
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
@@ -1802,6 +1854,7 @@ ias_status ias_plan::init(int dev, void *strm) {
         HIPC(hipEventCreateWithFlags(&join_ev[i], hipEventDisableTiming));
     }
     HIPC(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    for (auto &e : fix_ev) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     const char *e = getenv("IAS_SERIAL");
     serial = e && *e && *e != '0';
     HIPC(hipHostMalloc(&host_counters, 3 * sizeof(Counters)));   // [0], [1]: counters; [2]: A's base
@@ -1860,18 +1913,16 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     IAS_TRY(reserve(B_WSOFF, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(reserve(B_DUPOFF, sizeof(int64_t) * (rows + 1)));
     IAS_TRY(reserve(B_DUPN, sizeof(int32_t) * (rows + 1)));
-    IAS_TRY(reserve(B_CNT, sizeof(Counters)));
-    IAS_TRY(reserve(B_CNT2, sizeof(Counters)));
+    IAS_TRY(reserve(B_CNT, 2 * sizeof(Counters)));   // [0]: analysis / symbolic, [1]: numeric binning
     IAS_TRY(reserve(B_PTR, sizeof(int64_t) * (rows + 1)));
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
-    IAS_TRY(reserve(B_PART, sizeof(int64_t) * (nb + 2)));
+    IAS_TRY(reserve(B_PART, sizeof(int64_t) * (3 * nb + 4)));   // also the 3*rows scan of the num2 units
     Counters *dc = as<Counters>(bufs[B_CNT]);
-    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
 
     // ---- analysis: products per row, expanded A (+ product offsets), symbolic bin counts
     HIPC(hipEventRecord(ev[0], s));
-    HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
-    HIPC(hipMemsetAsync(dc2, 0, sizeof(Counters), s));
+    HIPC(hipMemsetAsync(dc, 0, 2 * sizeof(Counters), s));   // dc, dc2
     int32_t *axl = as<int32_t>(bufs[B_AXL]);
     int32_t *axr = as<int32_t>(bufs[B_AXR]);
     int64_t *axp = as<int64_t>(bufs[B_AXP]);
@@ -1909,18 +1960,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     hipStream_t s = (hipStream_t)stream;
     const BinSpec ss = sym_spec(), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
-    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
     Counters *hc = (Counters *)host_counters;
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
     const int64_t *axp = as<int64_t>(bufs[B_AXP]);
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
-    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    int64_t *a_base = (int64_t *)(hc + 2);
-    *a_base = 0;
-    if (A.ptr) HIPC(hipMemcpyAsync(a_base, A.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + A's base entry
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
-    ax_aval = A.val + *a_base;
+    ax_aval = A.val + (rows > 0 ? c1.a_base : 0);
     const AxView ax = ax_view();
     if (c1.overflow) {
         set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
@@ -2024,7 +2072,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // ---- row pointer of C, numeric binning by nnz (and products / nnz)
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
     IAS_TRY(reserve(B_NITEM, sizeof(PartItem) * (size_t)(rows + flops / NUM_PART_CAP + 2)));
-    n2_units = 0;
+    n2_units = n2_bunits = n2_dunits = 0;
     if (rows > 0) {
         k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
                                                           &dc2->max_nnz);
@@ -2032,34 +2080,46 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
     CHECK_LAUNCH("scan", s);
         k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
-                                                                    rows, ns, dc2);
+                                                                    rows, ns, dc2, ptr + rows);
         k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
             nullptr, dc2, nullptr, nullptr, 0);
     CHECK_LAUNCH("numeric binning", s);
-        if (num2_on()) {
+        // streaming rows exist only in the sym2 / partitioned bins (all rows
+        // short, as K1 / K2: no unit lists to build)
+        bool any_stream = c1.count[sym_part] > 0;
+        for (int b = 1; b <= ss.nval; ++b) {
+            const int32_t u = sym2 ? SYM2_BINS[b - 1].upper : SYM_BINS[b - 1].upper;
+            if (c1.count[b] > 0 && !(sym2 && u <= SHORT_MAX && short_on())) any_stream = true;
+        }
+        if (num2_on() && any_stream) {
             // work units of the row-unit numeric pass: 64 A entries of a streaming row
-            IAS_TRY(reserve(B_N2CNT, sizeof(int32_t) * (size_t)rows));
-            IAS_TRY(reserve(B_N2OFF, sizeof(int64_t) * (size_t)(rows + 1)));
+            // (ordered by class: rows with > 256 duplicates, with fewer,
+            // without — each class's fix-ups can start once its units are done)
+            IAS_TRY(reserve(B_N2CNT, sizeof(int32_t) * (size_t)(3 * rows)));
+            IAS_TRY(reserve(B_N2OFF, sizeof(int64_t) * (size_t)(3 * rows + 3)));
             IAS_TRY(reserve(B_N2UNIT, sizeof(Num2Unit) * (size_t)(rows + a_entries / N2_ENT + 1)));
             int32_t *cnt = as<int32_t>(bufs[B_N2CNT]);
             int64_t *uoff = as<int64_t>(bufs[B_N2OFF]);
             k_num2_count<<<grid_for(rows, 256), 256, 0, s>>>(A, rows, sa.dupn, as<int32_t>(bufs[B_PROD]), cnt);
-            scan_i32(cnt, rows, as<int64_t>(bufs[B_PART]), uoff, s);
-            k_num2_fill<<<grid_for(rows, 256), 256, 0, s>>>(rows, cnt, uoff, as<Num2Unit>(bufs[B_N2UNIT]));
+            scan_i32(cnt, 3 * rows, as<int64_t>(bufs[B_PART]), uoff, s);
+            k_num2_fill<<<grid_for(3 * rows, 256), 256, 0, s>>>(rows, cnt, uoff, as<Num2Unit>(bufs[B_N2UNIT]),
+                                                                 dc2);
             CHECK_LAUNCH("k_num2_fill", s);
-            HIPC(hipMemcpyAsync(&n2_units, uoff + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
         }
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[2], s));
-    HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    HIPC(hipMemcpyAsync(&nnz_total, ptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + nnz(C), unit counts
     HIPC(hipStreamSynchronize(s));
     const Counters c2 = hc[1];
+    nnz_total = rows > 0 ? (int64_t)c2.nnz_total : 0;
+    n2_units = (int64_t)c2.n2_units;
+    n2_bunits = (int64_t)c2.n2_bunits;
+    n2_dunits = (int64_t)c2.n2_dunits;
     if (c2.overflow) {
         set_last_error("hash partition table overflow in the symbolic pass");
         return IAS_ERROR_OVERFLOW;
@@ -2098,12 +2158,15 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     std::copy(num_count, num_count + MAX_BINS, cc.count);
     int64_t st[MAX_BINS];
     bin_starts(cc, st);
-    Counters *dc2 = as<Counters>(bufs[B_CNT2]);
+    Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
     const AxView ax = ax_view();
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
     HIPC(hipEventRecord(ev[3], s));
     int c;
+    std::function<ias_status(hipStream_t, int)> launch_fix;   // part 0: sorted fix-ups, 1: the others, 2: all
+    bool fix_split = false;
+    int fix_lane = 0, n2_launches = 0;
     // big bins first: their long rows start early and the small bins fill in behind
     IAS_TRY(fork());
     int lane_no = 0;
@@ -2135,41 +2198,85 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                           as<double>(bufs[B_DUPV])};
         const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
         const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 2048);
+        // fix-ups of the rows with duplicates: on the pass's stream after it,
+        // or (split) the 1024-lane sorted fix-ups (> 4096 duplicates) on the
+        // pass's stream right after their rows' units (they need whole CUs:
+        // beside the pass they would starve), the others on the next side
+        // stream once their class's units are done, beside the later units
+        const int fb = ns.nval + 3 + N_DW;
+        const bool fixups = num_count[fb] + num_count[fb + 1] + num_count[fb + 2] > 0;
+        // part 0: lists > 4096 (1024 lanes, whole CUs); 1: 1025 .. 4096; 2: the
+        // rest; 3: all
+        launch_fix = [&, fb](hipStream_t f, int part) -> ias_status {
+            int cf;
+            if ((part == 0 || part == 3) && (cf = num_count[fb + 2]) > 0) {
+                static bool fb_done = false;
+                allow_lds(k_fixup_big, fb_done, FIXBIG_LDS);
+                k_fixup_big<<<cf, 1024, FIXBIG_LDS, f>>>(NL + st[fb + 2], cf, bm, sa.dup_off, sa.dupn, sa.dupt,
+                                                         as<double>(bufs[B_DUPV]), out);
+                CHECK_LAUNCH("k_fixup_big", f);
+            }
+            if ((part == 1 || part == 3) && (cf = num_count[fb + 2]) > 0) {
+                static bool fl_done = false;
+                allow_lds(k_fixup_large, fl_done, FIXLARGE_LDS);
+                k_fixup_large<<<cf, 256, FIXLARGE_LDS, f>>>(NL + st[fb + 2], cf, bm, sa.dup_off, sa.dupn,
+                                                            sa.dupt, as<double>(bufs[B_DUPV]), out);
+                CHECK_LAUNCH("k_fixup_large", f);
+            }
+            if ((part == 2 || part == 3) && (cf = num_count[fb + 2]) > 0) {
+                k_fixup_mid<<<cf, 256, 0, f>>>(NL + st[fb + 2], cf, bm, sa.dup_off, sa.dupn, sa.dupt,
+                                               as<double>(bufs[B_DUPV]), out);
+                CHECK_LAUNCH("k_fixup_mid", f);
+            }
+            if ((part == 2 || part == 3) && (cf = num_count[fb]) > 0) {
+                k_fixup_tiny<<<grid_for(cf, 256), 256, 0, f>>>(NL + st[fb], cf, bm, sa.dup_off, sa.dupn, sa.dupt,
+                                                               as<double>(bufs[B_DUPV]), out);
+                CHECK_LAUNCH("k_fixup_tiny", f);
+            }
+            if ((part == 2 || part == 3) && (cf = num_count[fb + 1]) > 0) {
+                k_fixup<<<grid_for(cf, FIX_TPW), WAVE * FIX_TPW, 0, f>>>(NL + st[fb + 1], cf, bm, sa.dup_off,
+                                                                        sa.dupn, sa.dupt, as<double>(bufs[B_DUPV]),
+                                                                        out);
+                CHECK_LAUNCH("k_fixup", f);
+            }
+            return IAS_SUCCESS;
+        };
         HIPC(hipEventRecord(ev[5], t));
         if (num2_on()) {
             if (n2_units > 0) {
-                const Num2Args na{A, ax, fa.axp, fa.poff, B.col, B.val, as<Num2Unit>(bufs[B_N2UNIT]), n2_units,
-                                  bm, sa.dup_off, fa.dupval};
-                k_num2<<<(unsigned)((n2_units + N2_WPB - 1) / N2_WPB), 64 * N2_WPB, 0, t>>>(na, out);
+                Num2Args na{A, ax, fa.axp, fa.poff, B.col, B.val, as<Num2Unit>(bufs[B_N2UNIT]), n2_units,
+                            bm, sa.dup_off, fa.dupval};
+                fix_split = fixups && !serial && !small && n2_split_on();
+                // units by class: [0, bunits) rows with > 1024 duplicates,
+                // [bunits, dunits) with fewer, [dunits, units) without
+                const int64_t cut[4] = {0, fix_split ? n2_bunits : 0, fix_split ? n2_dunits : 0, n2_units};
+                for (int k = 0; k < 3; ++k) {
+                    const int64_t nu = cut[k + 1] - cut[k];
+                    if (nu > 0) {
+                        Num2Args nk = na;
+                        nk.units += cut[k];
+                        nk.nunits = nu;
+                        k_num2<<<(unsigned)((nu + N2_WPB - 1) / N2_WPB), 64 * N2_WPB, 0, t>>>(nk, out);
+                        ++n2_launches;
+                    }
+                    if (fix_split && k < 2) HIPC(hipEventRecord(fix_ev[k], t));
+                    if (fix_split && k == 0) IAS_TRY(launch_fix(t, 0));
+                }
+                fix_lane = lane_no;   // the fix-ups: the stream after this one
             }
         } else {
             k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
         }
         HIPC(hipEventRecord(ev[6], t));
         CHECK_LAUNCH("k_numeric_flat", t);
-        const int fb = ns.nval + 3 + N_DW;
-        if ((c = num_count[fb]) > 0) {
-            k_fixup_tiny<<<grid_for(c, 256), 256, 0, t>>>(NL + st[fb], c, bm, sa.dup_off, sa.dupn, sa.dupt,
-                                                          as<double>(bufs[B_DUPV]), out);
-            CHECK_LAUNCH("k_fixup_tiny", t);
-        }
-        if ((c = num_count[fb + 1]) > 0) {
-            k_fixup<<<grid_for(c, FIX_TPW), WAVE * FIX_TPW, 0, t>>>(NL + st[fb + 1], c, bm, sa.dup_off,
-                                                                   sa.dupn, sa.dupt, as<double>(bufs[B_DUPV]),
-                                                                   out);
-            CHECK_LAUNCH("k_fixup", t);
-        }
-        if ((c = num_count[fb + 2]) > 0) {
-            static bool fb_done = false;
-            allow_lds(k_fixup_big, fb_done, 8ull * FIXBIG_CAP);
-            k_fixup_big<<<c, 1024, 8ull * FIXBIG_CAP, t>>>(NL + st[fb + 2], c, bm, sa.dup_off, sa.dupn, sa.dupt,
-                                                           as<double>(bufs[B_DUPV]), out);
-            CHECK_LAUNCH("k_fixup_big", t);
-        }
+        if (!fix_split) IAS_TRY(launch_fix(t, 3));
     }
+    // short rows: all on the fix-up stream when the pass is split (ahead of
+    // its waits; not behind the streaming pass on a shared queue)
+    const int short_lane = fix_split ? fix_lane : -1;
     for (int i = 2; i >= 0 && ns.short_base > 0; --i)
         if ((c = num_count[ns.short_base + i]) > 0) {
-            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            hipStream_t t = (hipStream_t)side_stream(short_lane >= 0 ? short_lane : lane_no++);
             const ShortArgs sh{A, ax, B.col, B.val, NL + st[ns.short_base + i], c, nullptr, nullptr};
             short_num_launch(i, sh, out, t);
             CHECK_LAUNCH("k_short_num", t);
@@ -2180,6 +2287,13 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             val_bin(VAL_BINS[b - 1].cfg, Launch{c, slots_for(VAL_BINS[b - 1].upper), t, ax, B, NL + st[b]}, out);
             CHECK_LAUNCH("k_numeric_val", t);
         }
+    if (fix_split) {
+        hipStream_t f = (hipStream_t)side_stream(fix_lane);
+        HIPC(hipStreamWaitEvent(f, fix_ev[0], 0));
+        IAS_TRY(launch_fix(f, 1));
+        HIPC(hipStreamWaitEvent(f, fix_ev[1], 0));
+        IAS_TRY(launch_fix(f, 2));
+    }
     HIPC(hipGetLastError());
     IAS_TRY(join());
     if (out.row_idx && rows > 0)
@@ -2206,6 +2320,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         if (n_entries > 0 && hipEventElapsedTime(&f, ev[5], ev[6]) == hipSuccess) rep->ms_stream = f;
         rep->stream_products = st_prod;
         rep->stream_nnz = st_nnz;
+        rep->stream_launches = n2_launches;
     }
     return IAS_SUCCESS;
 }
@@ -2261,13 +2376,10 @@ ias_status ias_plan::onepass_prepare(const Rows &A, const Rows &B, int64_t rows,
         hi[0] = hi[1] = 0;
     }
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
-    int64_t *a_base = (int64_t *)(hc + 2);
-    *a_base = 0;
-    if (A.ptr) HIPC(hipMemcpyAsync(a_base, A.ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + A's base entry
     HIPC(hipStreamSynchronize(s));
     const Counters c1 = *hc;
-    ax_aval = A.val + *a_base;
+    ax_aval = A.val + (rows > 0 ? c1.a_base : 0);
     if (c1.overflow) {
         set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
         return IAS_ERROR_INVALID_ARGUMENT;

@@ -43,6 +43,9 @@ struct Counters {
     unsigned long long st_prod, st_nnz;   // products / C entries of the streaming rows
     unsigned long long items_cur, bm_cur, ws_cur, dup_cur;   // scatter-pass cursors
     unsigned long long part_prod, pb_cur;   // products of partitioned rows (bucket space) + cursor
+    unsigned long long nnz_total;           // nnz(C) (k_bin_count of the numeric binning)
+    long long a_base;                       // A's first entry (row_ptr[0]; k_an_rows)
+    unsigned long long n2_units, n2_bunits, n2_dunits;   // k_num2_fill: all units, class ends
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
@@ -104,6 +107,9 @@ struct ias_plan {
     unsigned long long num_items = 0;
     int64_t st_prod = 0, st_nnz = 0;
     int64_t n2_units = 0;   // work units of the row-unit numeric pass
+    int64_t n2_bunits = 0;  //   of which the first belong to rows with > 1024 duplicates,
+    int64_t n2_dunits = 0;  //   and up to here to rows with duplicates
+    hipEvent_t fix_ev[2] = {}; // units of class 0 / class 1 done: their fix-ups may start
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;

@@ -1118,13 +1118,18 @@ __device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows 
 
 // Fix-up of one streaming row with duplicates: each column's duplicate
 // products are added to its entry in product order (one lane per column).
+// The list and its values are staged in LDS first: the per-column walks then
+// read LDS, not one dependent global load per duplicate.
 template <int TEAM>
 __device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *bits, const uint32_t *bpref,
                                                   const int32_t *gdupt, const double *gdupval,
-                                                  int32_t ndup, int32_t *dupt, const Out &out) {
+                                                  int32_t ndup, int32_t *dupt, double *dval, const Out &out) {
     using TM = Team<TEAM>;
     const int lane = TM::lane();
-    for (int32_t i = lane; i < ndup; i += TEAM) dupt[i] = gdupt[i];
+    for (int32_t i = lane; i < ndup; i += TEAM) {
+        dupt[i] = gdupt[i];
+        dval[i] = gdupval[i];
+    }
     TM::sync();
     const int64_t st = out.start(row);
     const uint32_t nnz = (uint32_t)out.len[row];
@@ -1138,7 +1143,7 @@ __device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *b
         const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
         double v = out.val[pos];
         for (int32_t j = i; j < ndup; ++j)
-            if (dupt[j] == t) v = v + gdupval[j];
+            if (dupt[j] == t) v = v + dval[j];
         out.val[pos] = v;
     }
 }
@@ -1146,14 +1151,19 @@ __device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *b
 // Fix-up of a streaming row with many duplicates (more than one wave's
 // list): (first touch, index) keys sorted in LDS (bitonic, nd <= cap2 = a
 // power of two), then each run of equal first touches adds its products to
-// its entry in product order (sorted by index within the run).
-template <int TEAM>
+// its entry in product order (sorted by index within the run).  After the
+// sort every lane gathers its entries' values (independent loads, one round
+// of latency) into the key array's slots, run heads go to a bit mask, and the
+// runs are walked in LDS.
+template <int TEAM, int CAP>
 __device__ __forceinline__ void numeric_fixup_big(int64_t row, const uint32_t *bits, const uint32_t *bpref,
                                                   const int32_t *gdupt, const double *gdupval,
-                                                  int32_t ndup, unsigned long long *key, uint32_t cap2,
-                                                  const Out &out) {
+                                                  int32_t ndup, unsigned long long *key, const Out &out) {
     using TM = Team<TEAM>;
+    constexpr int PER = CAP / TEAM;
+    static_assert(PER * TEAM == CAP && TEAM % WAVE == 0, "whole waves over the key array");
     const int lane = TM::lane();
+    uint64_t *head = (uint64_t *)(key + CAP);   // CAP / 64 words
     uint32_t n2 = 1;
     while (n2 < (uint32_t)ndup) n2 <<= 1;
     for (uint32_t i = lane; i < n2; i += TEAM)
@@ -1174,19 +1184,107 @@ __device__ __forceinline__ void numeric_fixup_big(int64_t row, const uint32_t *b
             TM::sync();
         }
     }
+    uint32_t tt[PER];
+    double vv[PER];
+    bool hd[PER];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const uint32_t i = (uint32_t)(r * TEAM + lane);
+        const bool in = i < (uint32_t)ndup;
+        const unsigned long long kk = in ? key[i] : 0ull;
+        tt[r] = (uint32_t)(kk >> 32);
+        hd[r] = in && (i == 0 || (uint32_t)(key[i - 1] >> 32) != tt[r]);
+        vv[r] = in ? gdupval[(uint32_t)kk] : 0.0;
+    }
+    TM::sync();   // every key read before the values overwrite them
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        const uint32_t i = (uint32_t)(r * TEAM + lane);
+        const uint64_t hb = __ballot(hd[r]);
+        if (i < (uint32_t)ndup) key[i] = __builtin_bit_cast(unsigned long long, vv[r]);
+        if ((lane & (WAVE - 1)) == 0 && i < n2) head[i >> 6] = hb;
+    }
+    TM::sync();
+    const double *val = (const double *)key;
+    const int64_t st = out.start(row);
+    const uint32_t nnz = (uint32_t)out.len[row];
+#pragma unroll
+    for (int r = 0; r < PER; ++r) {
+        if (!hd[r]) continue;
+        const uint32_t i = (uint32_t)(r * TEAM + lane), t = tt[r];
+        const uint32_t rk = bpref[t >> 5] + (uint32_t)__popc(bits[t >> 5] & ((1u << (t & 31)) - 1u));
+        const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
+        double v = out.val[pos] + val[i];
+        for (uint32_t j = i + 1; j < (uint32_t)ndup && !((head[j >> 6] >> (j & 63)) & 1ull); ++j) v = v + val[j];
+        out.val[pos] = v;
+    }
+}
+
+// The same with the values staged in a second LDS array (16 B per list entry
+// in all, few registers): the 256-lane kernels that sit beside the streaming
+// pass's waves on a CU.  key: CAP keys, then CAP values, then CAP/64 head words.
+template <int TEAM, int CAP>
+__device__ __forceinline__ void numeric_fixup_lds(int64_t row, const uint32_t *bits, const uint32_t *bpref,
+                                                  const int32_t *gdupt, const double *gdupval,
+                                                  int32_t ndup, unsigned long long *key, const Out &out) {
+    using TM = Team<TEAM>;
+    static_assert(CAP % TEAM == 0 && TEAM % WAVE == 0, "whole waves over the key array");
+    const int lane = TM::lane();
+    double *val = (double *)(key + CAP);
+    uint64_t *head = (uint64_t *)(key + 2 * CAP);
+    uint32_t n2 = 1;
+    while (n2 < (uint32_t)ndup) n2 <<= 1;
+    for (uint32_t i = lane; i < n2; i += TEAM)
+        key[i] = i < (uint32_t)ndup ? (((unsigned long long)(uint32_t)gdupt[i] << 32) | i) : ~0ull;
+    TM::sync();
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < n2; i += TEAM) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = key[i], b = key[ixj];
+                    if ((a > b) == ((i & k) == 0)) {
+                        key[i] = b;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            TM::sync();
+        }
+    }
+    // run heads and the values in sorted order (the loads of a group of
+    // entries issued together)
+    constexpr int G = 4;
+    for (uint32_t i0 = 0; i0 < n2; i0 += G * TEAM) {
+        double v[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t i = i0 + g * TEAM + lane;
+            const bool in = i < (uint32_t)ndup;
+            const unsigned long long kk = in ? key[i] : 0ull;
+            const bool hd = in && (i == 0 || (uint32_t)(key[i - 1] >> 32) != (uint32_t)(kk >> 32));
+            const uint64_t hb = __ballot(hd);
+            if ((lane & (WAVE - 1)) == 0 && i < n2) head[i >> 6] = hb;
+            v[g] = in ? gdupval[(uint32_t)kk] : 0.0;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t i = i0 + g * TEAM + lane;
+            if (i < (uint32_t)ndup) val[i] = v[g];
+        }
+    }
+    TM::sync();
     const int64_t st = out.start(row);
     const uint32_t nnz = (uint32_t)out.len[row];
     for (uint32_t i = lane; i < (uint32_t)ndup; i += TEAM) {
+        if (!((head[i >> 6] >> (i & 63)) & 1ull)) continue;
         const uint32_t t = (uint32_t)(key[i] >> 32);
-        if (i > 0 && (uint32_t)(key[i - 1] >> 32) == t) continue;
         const uint32_t rk = bpref[t >> 5] + (uint32_t)__popc(bits[t >> 5] & ((1u << (t & 31)) - 1u));
         const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
-        double v = out.val[pos];
-        for (uint32_t j = i; j < (uint32_t)ndup && (uint32_t)(key[j] >> 32) == t; ++j)
-            v = v + gdupval[(uint32_t)key[j]];
+        double v = out.val[pos] + val[i];
+        for (uint32_t j = i + 1; j < (uint32_t)ndup && !((head[j >> 6] >> (j & 63)) & 1ull); ++j) v = v + val[j];
         out.val[pos] = v;
     }
-    (void)cap2;
 }
 
 // ---------------------------------------------------------------- numeric

@@ -32,9 +32,10 @@
 extern "C" {
 #endif
 
-#define IAS_ABI_VERSION 4   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
+#define IAS_ABI_VERSION 5   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
                                3: ias_csr_mul_csr_into (single pass);
-                               4: input-aware selector (features, images, MatNet) */
+                               4: input-aware selector (features, images, MatNet);
+                               5: ias_report.stream_launches */
 
 typedef enum ias_status {
     IAS_SUCCESS = 0,
@@ -136,11 +137,15 @@ typedef struct ias_report {
     int64_t nnz_c;
     int64_t max_row_products;
     int64_t max_row_nnz;
-    /* the step's largest launch, k_numeric_flat (streaming rows: C written
-       without a hash table), timed with events on its own stream */
+    /* the step's largest pass, the streaming numeric pass (k_num2: rows
+       resolved by the symbolic bitmap, C written without a hash table), timed
+       with events on its own stream */
     double  ms_stream;
     int64_t stream_products; /* products it processed */
     int64_t stream_nnz;      /* entries of C it wrote */
+    int32_t stream_launches; /* its launches: 2 when the rows with duplicates go
+                                first and their fix-ups overlap the rest */
+    int32_t reserved1;
 } ias_report;
 
 typedef struct ias_mtx_info {

@@ -143,12 +143,15 @@ def duplicate_tiers(seed=11):
     takes m_i distinct rows of its own group of B, whose 100 columns are drawn
     from a pool sized for the wanted duplicate count (d ~ P^2 / 2 pool):
       P=1000 ~30 dups (one-wave fix-up), P=8000 ~500 (sorted fix-up, LDS bin),
-      P=30000 ~1800 (partitioned row, streaming), P=20000 ~5000 (partitioned
-      row beyond its list: table path), P=2000 ~500 (LDS row beyond its list:
-      direct-write table); then 2000 ordinary rows."""
+      P=30000 ~1700 (partitioned row, streaming, 256-lane sorted fix-up),
+      P=20000 ~4300 (partitioned row, streaming: list cap P/4), P=2000 ~500
+      (LDS row beyond its list: direct-write table), P=30000 ~5300
+      (partitioned, streaming, the 1024-lane sorted fix-up), P=20000 ~6200
+      (partitioned row beyond its list: table path); then 2000 ordinary rows."""
     rng = np.random.default_rng(seed)
     per = 100
-    plan = [(1000, 16000), (8000, 64000), (30000, 250000), (20000, 40000), (2000, 3333)]
+    plan = [(1000, 16000), (8000, 64000), (30000, 250000), (20000, 40000), (2000, 3333), (30000, 75000),
+            (20000, 25000)]
     brows, arows = [], []
     ncols = 300000
     for prods, pool in plan:
