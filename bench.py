@@ -284,9 +284,10 @@ def main(argv=None):
         kname = "k_onepass" if args.engine == "onepass" else \
             ("k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2")
         units = {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)}
-        # the pass is 1 or 2 launches (rows with duplicates first, their fix-ups
-        # then overlap the rest): per launch = the pass's bytes and time / launches,
-        # which is what rocprofv3's average launch duration of the kernel shows
+        # the pass is 1 to 3 launches (rows by duplicate class; each class's
+        # fix-ups overlap the rest): ms_stream sums the launches' own durations
+        # (events around each launch), so per launch = the pass's bytes and time
+        # / launches, which is what rocprofv3's average launch duration shows
         launches = max(1, int(getattr(rep, "stream_launches", 1) or 1))
         if args.engine == "twophase" and int(rep.stream_nnz) < local_nnz // 2:
             # most of C comes from the short-row / table kernels (K1, K2): the

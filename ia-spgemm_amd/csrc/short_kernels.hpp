@@ -30,6 +30,9 @@ namespace ias {
 namespace dev {
 
 constexpr int SH_WPB = 4;   // waves (rows) per workgroup
+#ifndef SH_ST_EARLY
+#define SH_ST_EARLY 1   // numeric: C's row start loaded with the row's A entries
+#endif
 #ifndef SH_STAGE
 #define SH_STAGE 1   // numeric: C staged in LDS, 16-byte stores
 #endif
@@ -233,10 +236,20 @@ __global__ __launch_bounds__(64 * SH_WPB) void k_short_num(ShortArgs a, Out out)
     const uint64_t lt = (1ull << lane) - 1ull;
     RowRef ref = sh_ref(a, idx);
     ShEnt en = sh_load<true>(a, ref, true);
+    // C's row start is loaded with the row's A entries (not after the table
+    // work: one dependent global load less per row)
+#if SH_ST_EARLY
+    int64_t st = out.start(ref.row);
+#endif
     RowRef nref = sh_ref(a, idx + stride);
     while (idx < a.count) {
         const bool nvalid = idx + stride < a.count;
         const ShEnt nen = sh_load<true>(a, nref, nvalid);
+#if SH_ST_EARLY
+        const int64_t nst = nvalid ? out.start(nref.row) : 0;
+#else
+        const int64_t st = out.start(ref.row);
+#endif
         const RowRef nnref = sh_ref(a, idx + 2 * stride);
         int32_t c[K];
         double pv[K];
@@ -288,7 +301,6 @@ __global__ __launch_bounds__(64 * SH_WPB) void k_short_num(ShortArgs a, Out out)
                     }
             }
         }
-        const int64_t st = out.start(ref.row);
 #if SH_STAGE
         // The row's C entries staged by position in the table's LDS (no longer
         // needed: the next row re-initialises it) and written as ascending
@@ -353,6 +365,9 @@ __global__ __launch_bounds__(64 * SH_WPB) void k_short_num(ShortArgs a, Out out)
 #endif
         ref = nref;
         en = nen;
+#if SH_ST_EARLY
+        st = nst;
+#endif
         nref = nnref;
         idx += stride;
     }

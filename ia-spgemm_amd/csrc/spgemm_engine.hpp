@@ -110,6 +110,7 @@ struct ias_plan {
     int64_t n2_bunits = 0;  //   of which the first belong to rows with > 1024 duplicates,
     int64_t n2_dunits = 0;  //   and up to here to rows with duplicates
     hipEvent_t fix_ev[2] = {}; // units of class 0 / class 1 done: their fix-ups may start
+    hipEvent_t n2_ev[6] = {};  // around each streaming-pass launch: ms_stream = their sum
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;

@@ -139,12 +139,12 @@ typedef struct ias_report {
     int64_t max_row_nnz;
     /* the step's largest pass, the streaming numeric pass (k_num2: rows
        resolved by the symbolic bitmap, C written without a hash table), timed
-       with events on its own stream */
+       with events on its own stream (the sum of its launches' durations) */
     double  ms_stream;
     int64_t stream_products; /* products it processed */
     int64_t stream_nnz;      /* entries of C it wrote */
-    int32_t stream_launches; /* its launches: 2 when the rows with duplicates go
-                                first and their fix-ups overlap the rest */
+    int32_t stream_launches; /* its launches: up to 3 (rows by duplicate class,
+                                each class's fix-ups overlapping the rest) */
     int32_t reserved1;
 } ias_report;
 
