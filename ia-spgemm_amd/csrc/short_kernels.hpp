@@ -213,14 +213,134 @@ __global__ __launch_bounds__(64 * SH_WPB) void k_short_sym(ShortArgs a) {
     }
 }
 
+// R rows per wave (symbolic): the rows' staging, gathers and first probes are
+// issued together, so one wave keeps R rows' dependent chains (list -> A
+// entries -> B columns -> LDS CAS) in flight instead of one.
+template <int K, int R, bool NUM>
+__device__ __forceinline__ void short_gather_r(const ShortArgs &a, ShortLds<K, NUM> (&L)[R], const ShEnt (&en)[R],
+                                               int32_t (&c)[R][K], double (&pv)[R][K], int32_t (&P)[R]) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    int rel[R];
+    uint64_t ne[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (lane < K) L[r].wmask[lane] = 0ull;
+        const int incl = wave_incl_sum(en[r].bl);
+        rel[r] = incl - en[r].bl;
+        P[r] = __builtin_amdgcn_readlane(incl, WAVE - 1);
+        ne[r] = __ballot(en[r].bl > 0);
+    }
+    sh_wave_sync();   // wmask cleared
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (en[r].bl > 0) {
+            const int o = __popcll(ne[r] & ((1ull << lane) - 1ull));
+            L[r].ebs[o] = en[r].bs - rel[r];
+            if (NUM) L[r].eav[o] = en[r].av;
+            atomicOr(&L[r].wmask[rel[r] >> 6], 1ull << (rel[r] & 63));
+        }
+    sh_wave_sync();
+    const uint64_t upto = (2ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int before = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const unsigned long long m = L[r].wmask[k];
+            const int32_t p = 64 * k + lane;
+            const int e = max(before + __popcll(m & upto) - 1, 0);
+            const bool in = p < P[r];
+            const int64_t kb = in ? L[r].ebs[e] + p : 0;
+            c[r][k] = in ? a.bcol[kb] : SH_EMPTY;
+            pv[r][k] = 0.0;
+            if (NUM) pv[r][k] = in ? L[r].eav[e] * a.bval[kb] : 0.0;
+            before += __popcll(m);
+        }
+    }
+}
+
+// sh_insert over R tables: every item's first probe is issued before any
+// collision is chased.
+template <int S, int K, int R, typename T>
+__device__ __forceinline__ void sh_insert_r(T (&L)[R], const int32_t (&c)[R][K], uint32_t (&slot)[R][K],
+                                            int (&made)[R]) {
+    constexpr int LG = __builtin_ctz(S);
+    int32_t g[R][K];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            slot[r][k] = sh_hash(c[r][k], LG);
+            g[r][k] = atomicCAS(&L[r].keys[slot[r][k]], SH_EMPTY, c[r][k]);
+        }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        made[r] = 0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (c[r][k] == SH_EMPTY) continue;
+            if (g[r][k] == SH_EMPTY) {
+                ++made[r];
+                continue;
+            }
+            uint32_t s = slot[r][k];
+            for (int probe = 1; probe < S && g[r][k] != c[r][k]; ++probe) {
+                s = (s + 1) & (S - 1);
+                g[r][k] = atomicCAS(&L[r].keys[s], SH_EMPTY, c[r][k]);
+                if (g[r][k] == SH_EMPTY) {
+                    ++made[r];
+                    break;
+                }
+            }
+            slot[r][k] = s;
+        }
+    }
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(64 * SH_WPB) void k_short_sym_r(ShortArgs a) {
+    using LDS = ShortLds<K, false>;
+    __shared__ LDS lds[SH_WPB][R];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int64_t idx = ((int64_t)blockIdx.x * SH_WPB + w) * R;
+    if (idx >= a.count) return;
+    LDS(&L)[R] = lds[w];
+    RowRef ref[R];
+    ShEnt en[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        for (int i = lane; i < LDS::S; i += WAVE) L[r].keys[i] = SH_EMPTY;
+        ref[r] = sh_ref(a, idx + r);
+        en[r] = sh_load<false>(a, ref[r], idx + r < a.count);
+    }
+    int32_t c[R][K], P[R];
+    double pv[R][K];
+    short_gather_r<K, R, false>(a, L, en, c, pv, P);
+    uint32_t slot[R][K];
+    int made[R];
+    sh_insert_r<LDS::S, K, R>(L, c, slot, made);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int nnz = __builtin_amdgcn_readlane(wave_incl_sum(made[r]), WAVE - 1);
+        if (lane == 0 && idx + r < a.count) {
+            a.nnz_row[ref[r].row] = nnz;
+            a.dupn[ref[r].row] = P[r] - nnz > SH_DUP_MAX ? -1 : -5;
+        }
+    }
+}
+
 __device__ __forceinline__ double sh_readlane(double v, int l) {
     const uint64_t u = __builtin_bit_cast(uint64_t, v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+#ifndef SH_NUM_WPE
+#define SH_NUM_WPE 1   // minimum waves per SIMD the register allocation must allow (A/B knob)
+#endif
 template <int K>
-__global__ __launch_bounds__(64 * SH_WPB) void k_short_num(ShortArgs a, Out out) {
+__global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_NUM_WPE))) void k_short_num(ShortArgs a, Out out) {
     using LDS = ShortLds<K, true>;
     __shared__ LDS lds[SH_WPB];
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));

@@ -1590,7 +1590,23 @@ static unsigned short_grid(F kern, int32_t count) {
     if (!persist) return (unsigned)std::max<int64_t>(1, want);
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, resident_blocks(kern, 64 * SH_WPB, 0)));
 }
+// SH_SYM_R rows per wave in the short symbolic pass (1: the persistent
+// one-row kernel above)
+#ifndef SH_SYM_R
+#define SH_SYM_R 2
+#endif
+static unsigned short_grid_r(int32_t count, int r) {
+    return (unsigned)std::max<int64_t>(1, ((int64_t)count + SH_WPB * r - 1) / (SH_WPB * r));
+}
 static void short_sym_launch(int32_t upper, const ShortArgs &a, hipStream_t t) {
+    if (SH_SYM_R > 1) {
+        constexpr int R = SH_SYM_R > 1 ? SH_SYM_R : 2;
+        const unsigned g = short_grid_r(a.count, R);
+        if (upper <= 64) k_short_sym_r<1, R><<<g, 64 * SH_WPB, 0, t>>>(a);
+        else if (upper <= 128) k_short_sym_r<2, R><<<g, 64 * SH_WPB, 0, t>>>(a);
+        else k_short_sym_r<4, R><<<g, 64 * SH_WPB, 0, t>>>(a);
+        return;
+    }
     if (upper <= 64) k_short_sym<1><<<short_grid(k_short_sym<1>, a.count), 64 * SH_WPB, 0, t>>>(a);
     else if (upper <= 128) k_short_sym<2><<<short_grid(k_short_sym<2>, a.count), 64 * SH_WPB, 0, t>>>(a);
     else k_short_sym<4><<<short_grid(k_short_sym<4>, a.count), 64 * SH_WPB, 0, t>>>(a);
