@@ -215,7 +215,10 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
 }
 
 constexpr int BIN_BLOCK = 256;
-constexpr int BIN_RPT = 8;                       // rows per thread of the row passes
+#ifndef BIN_RPT_DEF
+#define BIN_RPT_DEF 8
+#endif
+constexpr int BIN_RPT = BIN_RPT_DEF;             // rows per thread of the row passes
 constexpr int BIN_ROWS = BIN_BLOCK * BIN_RPT;    // rows per block
 
 __device__ __forceinline__ int32_t ent2_of(const BinSpec &sp, const Rows &A, int64_t r) {
