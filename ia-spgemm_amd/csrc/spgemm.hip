@@ -1374,7 +1374,13 @@ struct BinCfg {
 static constexpr BinCfg SYM_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {1024, 4},
                                       {1536, 5}, {2048, 5}, {2730, 5}, {3640, 6}, {4550, 6},
                                       {5460, 6}, {7280, 7}, {9100, 7}, {SYM_MAX, 7}};
-static constexpr BinCfg VAL_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
+// value-table config of the <= 16-entry bin: 8-lane teams, 4 products per
+// lane (K1: 101 vs 130 us with 16-lane teams; 32- / 64-lane teams 214 / 254
+// us; 8 products per lane 171 us)
+#ifndef VAL_CFG16
+#define VAL_CFG16 9
+#endif
+static constexpr BinCfg VAL_BINS[] = {{16, VAL_CFG16},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
                                       {512, 4},  {768, 5},  {1024, 5}, {1365, 5}, {1820, 6},
                                       {2430, 6}, {3240, 7}, {4320, 7}, {VAL_MAX, 7}};
 static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},   {256, 3},
@@ -1465,7 +1471,7 @@ static constexpr int32_t dcap_for(int32_t upper) {
 
 // TEAM * PER of each value configuration in val_bin(): the emission loop
 // visits that many slots, so it must cover every bin's S.
-static constexpr uint32_t VAL_CFG_EMIT[] = {48, 96, 192, 384, 768, 2048, 4096, 8192};
+static constexpr uint32_t VAL_CFG_EMIT[] = {48, 96, 192, 384, 768, 2048, 4096, 8192, 48, 48, 48};
 static constexpr bool val_bins_covered() {
     for (int i = 0; i < N_VAL; ++i)
         if (VAL_CFG_EMIT[VAL_BINS[i].cfg] < slots_for(VAL_BINS[i].upper)) return false;
@@ -1753,6 +1759,9 @@ static void val_bin(int cfg, const Launch &l, const Out &out) {
         case 4: val_launch<128, 4, 128, 1, 6>(l, out); break;
         case 5: val_launch<256, 4, 256, 1, 8>(l, out); break;
         case 6: val_launch<512, 4, 256, 1, 8>(l, out); break;
+        case 8: val_launch<8, 8, 8, 32, 6>(l, out); break;   // VAL_CFG16 A/B: 8-lane teams
+        case 9: val_launch<8, 4, 8, 32, 6>(l, out); break;
+        case 10: val_launch<4, 4, 4, 64, 12>(l, out); break;
         default: val_launch<1024, 2, 256, 1, 8>(l, out); break;
     }
 }
