@@ -33,6 +33,9 @@ constexpr int SH_WPB = 4;   // waves (rows) per workgroup
 #ifndef SH_ST_EARLY
 #define SH_ST_EARLY 1   // numeric: C's row start loaded with the row's A entries
 #endif
+#ifndef SH_NODUP
+#define SH_NODUP 1   // numeric: rows without duplicates written straight from the gather
+#endif
 #ifndef SH_STAGE
 #define SH_STAGE 1   // numeric: C staged in LDS, 16-byte stores
 #endif
@@ -361,10 +364,12 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
 #if SH_ST_EARLY
     int64_t st = out.start(ref.row);
 #endif
+    int32_t rn = out.len[ref.row];   // the row's nnz (symbolic pass)
     RowRef nref = sh_ref(a, idx + stride);
     while (idx < a.count) {
         const bool nvalid = idx + stride < a.count;
         const ShEnt nen = sh_load<true>(a, nref, nvalid);
+        const int32_t nrn = nvalid ? out.len[nref.row] : 0;
 #if SH_ST_EARLY
         const int64_t nst = nvalid ? out.start(nref.row) : 0;
 #else
@@ -373,7 +378,34 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
         const RowRef nnref = sh_ref(a, idx + 2 * stride);
         int32_t c[K];
         double pv[K];
-        short_gather<K, true>(a, L, en, c, pv);
+        const int32_t P = short_gather<K, true>(a, L, en, c, pv);
+#if SH_NODUP
+        if (rn == P) {
+            // no duplicates (nnz = products): every product is its column's
+            // first touch, rank = product index — C is the products in reverse
+            // (forward for COO) order, each 0.0 + a*b (a*b); no table
+#if !SH_ST_EARLY
+            const int64_t st = out.start(ref.row);
+#endif
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (c[k] != SH_EMPTY) {
+                    const int32_t p = 64 * k + lane;
+                    const int64_t pos = st + (out.order == 0 ? P - 1 - p : p);
+                    __builtin_nontemporal_store(c[k], &out.col[pos]);
+                    __builtin_nontemporal_store(out.first_assign ? pv[k] : 0.0 + pv[k], &out.val[pos]);
+                }
+            ref = nref;
+            en = nen;
+            rn = nrn;
+#if SH_ST_EARLY
+            st = nst;
+#endif
+            nref = nnref;
+            idx += stride;
+            continue;
+        }
+#endif
         uint32_t slot[K];
         sh_insert<LDS::S, K>(L.keys, c, slot);
 #pragma unroll
@@ -485,6 +517,7 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
 #endif
         ref = nref;
         en = nen;
+        rn = nrn;
 #if SH_ST_EARLY
         st = nst;
 #endif
