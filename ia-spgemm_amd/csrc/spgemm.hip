@@ -220,6 +220,20 @@ constexpr int BIN_BLOCK = 256;
 #endif
 constexpr int BIN_RPT = BIN_RPT_DEF;             // rows per thread of the row passes
 constexpr int BIN_ROWS = BIN_BLOCK * BIN_RPT;    // rows per block
+// Small row counts use BIN_RPT / 2 rows per thread (twice the blocks: K1's
+// 256k rows 128 -> 256 blocks; its binning 0.354 -> 0.337 ms per step); from
+// BIN_RPT_BIG_ROWS rows on BIN_RPT (K2 / K3': 4 measured 1 % slower).
+#ifndef BIN_RPT_BIG_ROWS
+#define BIN_RPT_BIG_ROWS (1 << 20)
+#endif
+constexpr int BIN_RPT_SMALL = BIN_RPT > 1 ? BIN_RPT / 2 : 1;
+#define BIN_LAUNCH(kern, nrows, strm, ...)                                                                       \
+    do {                                                                                                         \
+        if ((nrows) < BIN_RPT_BIG_ROWS)                                                                          \
+            kern<BIN_RPT_SMALL><<<grid_for((nrows), BIN_BLOCK * BIN_RPT_SMALL), BIN_BLOCK, 0, (strm)>>>(__VA_ARGS__); \
+        else                                                                                                     \
+            kern<BIN_RPT><<<grid_for((nrows), BIN_ROWS), BIN_BLOCK, 0, (strm)>>>(__VA_ARGS__);                   \
+    } while (0)
 
 __device__ __forceinline__ int32_t ent2_of(const BinSpec &sp, const Rows &A, int64_t r) {
     if (!sp.ent_key) return 0;
@@ -229,14 +243,15 @@ __device__ __forceinline__ int32_t ent2_of(const BinSpec &sp, const Rows &A, int
     return n > INT32_MAX / sp.ent_key ? INT32_MAX : sp.ent_key * n;
 }
 
+template <int RPT>
 __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int64_t rows, int32_t *prod,
                                                        BinSpec spec, Counters *cnt, Rows A) {
-    int b[BIN_RPT];
-    int32_t k[BIN_RPT];
+    int b[RPT];
+    int32_t k[RPT];
     int mx = 0;
 #pragma unroll
-    for (int i = 0; i < BIN_RPT; ++i) {
-        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + threadIdx.x;
+    for (int i = 0; i < RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * (BIN_BLOCK * RPT) + i * BIN_BLOCK + threadIdx.x;
         b[i] = -1;
         k[i] = 0;
         if (r < rows) {
@@ -247,7 +262,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
             mx = max(mx, k[i]);
         }
     }
-    count_bins<BIN_BLOCK, BIN_RPT>(spec, b, k, cnt);
+    count_bins<BIN_BLOCK, RPT>(spec, b, k, cnt);
 #pragma unroll
     for (int d = WAVE / 2; d > 0; d >>= 1) mx = max(mx, __shfl_xor(mx, d));
     __shared__ int wmx[BIN_BLOCK / WAVE];
@@ -266,17 +281,18 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
 // Counting pass of a binning (numeric and sort binnings; the symbolic one is
 // fused into k_an_rows).  prod may be null (class test off); a row is
 // streaming-class when stn is given and stn[r] >= 0.
+template <int RPT>
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, const int32_t *prod,
                                                          const int32_t *stn, int64_t rows,
                                                          BinSpec spec, Counters *cnt,
                                                          const int64_t *total = nullptr) {
     if (total && blockIdx.x == 0 && threadIdx.x == 0) cnt->nnz_total = (unsigned long long)*total;
-    int b[BIN_RPT];
-    int32_t k[BIN_RPT];
+    int b[RPT];
+    int32_t k[RPT];
     unsigned long long sp = 0, sn = 0;
 #pragma unroll
-    for (int i = 0; i < BIN_RPT; ++i) {
-        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + threadIdx.x;
+    for (int i = 0; i < RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * (BIN_BLOCK * RPT) + i * BIN_BLOCK + threadIdx.x;
         b[i] = -1;
         k[i] = 0;
         if (r < rows) {
@@ -290,7 +306,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
             }
         }
     }
-    count_bins<BIN_BLOCK, BIN_RPT>(spec, b, k, cnt);
+    count_bins<BIN_BLOCK, RPT>(spec, b, k, cnt);
     if (stn) {   // block sums, one pair of atomics per block
         __shared__ unsigned long long red[2][BIN_BLOCK / WAVE];
         for (int d = WAVE / 2; d > 0; d >>= 1) {
@@ -322,6 +338,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_count(const int32_t *key, con
 // FT); global-table rows a workspace offset of nextpow2(ceil(k*3/2)) slots.
 // R rows per thread; per-row allocations come from a block prefix and one
 // cursor atomic per block and counter.
+template <int RPT>
 __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, const int32_t *prod,
                                                            const int32_t *stn, int64_t rows,
                                                            BinSpec spec, Rows A, RowRef *lists,
@@ -346,12 +363,12 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
     }
     __syncthreads();
     const int part_bin = spec.nval + 1, wide_bin = spec.nval + 2;
-    int b[BIN_RPT], local[BIN_RPT];
-    int32_t k[BIN_RPT];
+    int b[RPT], local[RPT];
+    int32_t k[RPT];
     unsigned long long mine[NQ] = {0ull, 0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-    for (int i = 0; i < BIN_RPT; ++i) {
-        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
+    for (int i = 0; i < RPT; ++i) {
+        const int64_t r = (int64_t)blockIdx.x * (BIN_BLOCK * RPT) + i * BIN_BLOCK + t;
         b[i] = -1;
         local[i] = 0;
         k[i] = 0;
@@ -380,9 +397,9 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_bin_scatter(const int32_t *key, c
 #pragma unroll
     for (int j = 0; j < NQ; ++j) at[j] += cbase[j];
 #pragma unroll
-    for (int i = 0; i < BIN_RPT; ++i) {
+    for (int i = 0; i < RPT; ++i) {
         if (b[i] <= 0) continue;
-        const int64_t r = (int64_t)blockIdx.x * BIN_ROWS + i * BIN_BLOCK + t;
+        const int64_t r = (int64_t)blockIdx.x * (BIN_BLOCK * RPT) + i * BIN_BLOCK + t;
         unsigned long long n[NQ];
         bin_needs(spec, b[i], k[i], n);
         const int64_t within = base[b[i]] + local[i];
@@ -1599,10 +1616,14 @@ static unsigned short_grid(F kern, int32_t count) {
     if (!persist) return (unsigned)std::max<int64_t>(1, want);
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, resident_blocks(kern, 64 * SH_WPB, 0)));
 }
-// SH_SYM_R rows per wave in the short symbolic pass (1: the persistent
-// one-row kernel above)
+// SH_SYM_R rows per wave in the short symbolic pass for rows of <= 128
+// products (1: the one-row kernel below); rows of 129..256 products one per
+// wave with the 4-slots-per-product table (SH_SYM_R4 = 2: two per wave)
 #ifndef SH_SYM_R
 #define SH_SYM_R 2
+#endif
+#ifndef SH_SYM_R4
+#define SH_SYM_R4 1
 #endif
 static unsigned short_grid_r(int32_t count, int r) {
     return (unsigned)std::max<int64_t>(1, ((int64_t)count + SH_WPB * r - 1) / (SH_WPB * r));
@@ -1613,7 +1634,8 @@ static void short_sym_launch(int32_t upper, const ShortArgs &a, hipStream_t t) {
         const unsigned g = short_grid_r(a.count, R);
         if (upper <= 64) k_short_sym_r<1, R><<<g, 64 * SH_WPB, 0, t>>>(a);
         else if (upper <= 128) k_short_sym_r<2, R><<<g, 64 * SH_WPB, 0, t>>>(a);
-        else k_short_sym_r<4, R><<<g, 64 * SH_WPB, 0, t>>>(a);
+        else if (SH_SYM_R4 > 1) k_short_sym_r<4, R><<<g, 64 * SH_WPB, 0, t>>>(a);
+        else k_short_sym<4><<<short_grid(k_short_sym<4>, a.count), 64 * SH_WPB, 0, t>>>(a);
         return;
     }
     if (upper <= 64) k_short_sym<1><<<short_grid(k_short_sym<1>, a.count), 64 * SH_WPB, 0, t>>>(a);
@@ -1978,7 +2000,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     }
     k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff, dc);
     if (rows > 0)
-        k_an_rows<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
+        BIN_LAUNCH(k_an_rows, rows, s, poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
     CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
@@ -2040,7 +2062,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     RowRef *SL = as<RowRef>(bufs[B_SLIST]);
     int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
     if (rows > 0)
-        k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
+        BIN_LAUNCH(k_bin_scatter, rows, s, 
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
             as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc, as<int64_t>(bufs[B_PFIRST]),
             as<int64_t>(bufs[B_PBOFF]), sym2 ? 1 : 0);
@@ -2110,9 +2132,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART]), nb);
         k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]), ptr);
     CHECK_LAUNCH("scan", s);
-        k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
+        BIN_LAUNCH(k_bin_count, rows, s, nnz, as<int32_t>(bufs[B_PROD]), sa.dupn,
                                                                     rows, ns, dc2, ptr + rows);
-        k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(
+        BIN_LAUNCH(k_bin_scatter, rows, s, 
             nnz, as<int32_t>(bufs[B_PROD]), sa.dupn, rows, ns, A, as<RowRef>(bufs[B_NLIST]),
             as<PartItem>(bufs[B_NITEM]), nullptr, as<int64_t>(bufs[B_WSOFF]), nullptr, nullptr, nullptr,
             nullptr, dc2, nullptr, nullptr, 0);
@@ -2579,8 +2601,8 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
     // the scatter's row extents are not used by the sort kernels (they read ptr/len)
     const Rows span{ptr, len, stride, nullptr, nullptr};
-    k_bin_count<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, dc);
-    k_bin_scatter<<<grid_for(rows, BIN_ROWS), BIN_BLOCK, 0, s>>>(len, nullptr, nullptr, rows, spec, span,
+    BIN_LAUNCH(k_bin_count, rows, s, len, nullptr, nullptr, rows, spec, dc);
+    BIN_LAUNCH(k_bin_scatter, rows, s, len, nullptr, nullptr, rows, spec, span,
                                                                   lists, nullptr, nullptr, offs, nullptr,
                                                                   nullptr, nullptr, nullptr, dc, nullptr, nullptr, 0);
     Counters hc;
