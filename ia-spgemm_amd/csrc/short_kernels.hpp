@@ -33,6 +33,12 @@ constexpr int SH_WPB = 4;   // waves (rows) per workgroup
 #ifndef SH_ST_EARLY
 #define SH_ST_EARLY 1   // numeric: C's row start loaded with the row's A entries
 #endif
+#ifndef SH_SYM_SF12
+#define SH_SYM_SF12 2   // A/B knobs: symbolic slots for K = 1, 2 rows; numeric for K = 4
+#endif
+#ifndef SH_NUM_SF4
+#define SH_NUM_SF4 2
+#endif
 #ifndef SH_SYM_SF4
 #define SH_SYM_SF4 4   // symbolic table slots per product bound, K = 4 rows
 #endif
@@ -64,7 +70,7 @@ struct ShortLds {
     // table slots: 2 per product bound; the symbolic pass's 256-product rows
     // 4 (shorter probe chains: K2 symbolic 1.01 -> 0.79 ms with one row per
     // wave — two rows per wave then need 8.5 KB of LDS per wave, 1.05 ms)
-    static constexpr int S = (NUM ? 2 : (K >= 4 ? SH_SYM_SF4 : 2)) * P;
+    static constexpr int S = (NUM ? (K >= 4 ? SH_NUM_SF4 : 2) : (K >= 4 ? SH_SYM_SF4 : SH_SYM_SF12)) * P;
     __attribute__((aligned(16))) int32_t keys[S];
     __attribute__((aligned(16))) int32_t minp[NUM ? S : 4];   // numeric: first product of the slot's column
     int64_t ebs[SH_ENT];         // non-empty entries: B-row start - row-relative first product
