@@ -184,7 +184,10 @@ __device__ __forceinline__ int sh_insert(int32_t *keys, const int32_t (&c)[K], u
 // Rows with more duplicates than this take the table path (dupn -1: the
 // numeric LDS value / direct-write bins), which adds them in parallel; the
 // short numeric pass adds duplicates one at a time.
-constexpr int SH_DUP_MAX = 16;
+#ifndef SH_DUP_MAX_DEF
+#define SH_DUP_MAX_DEF 16
+#endif
+constexpr int SH_DUP_MAX = SH_DUP_MAX_DEF;
 
 // Persistent waves (grid-stride over the bin's rows); the next row's list
 // entry and A entries are loaded while this row is resolved.
