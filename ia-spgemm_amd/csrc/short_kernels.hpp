@@ -185,7 +185,7 @@ __device__ __forceinline__ int sh_insert(int32_t *keys, const int32_t (&c)[K], u
 // numeric LDS value / direct-write bins), which adds them in parallel; the
 // short numeric pass adds duplicates one at a time.
 #ifndef SH_DUP_MAX_DEF
-#define SH_DUP_MAX_DEF 16
+#define SH_DUP_MAX_DEF 8   // K1 numeric 0.097 vs 0.103 ms with 16 (32: 0.103); K3' within noise
 #endif
 constexpr int SH_DUP_MAX = SH_DUP_MAX_DEF;
 
