@@ -10,8 +10,10 @@
 //     C[i][slot] = ((0.0 + A[i][ja0]*B[i+a0][kb0]) + A[i][ja1]*B[i+a1][kb1]) ...
 // reproduces the reference's sums bit for bit (-ffp-contract=off).  One lane
 // per element makes the C store fully coalesced (row-major rows x nd_C); A
-// and B rows are re-read from L2 by the nd_C lanes of a row.  The kernel is
-// HBM-bound (~0.4 flop/byte at 7 diagonals), so no MFMA: DESIGN.md §DIA.
+// and B rows are re-read from L2 by the nd_C lanes of a row (k_dia_mul; the
+// tiled form k_dia_tile stages them in LDS).  Narrow bands are HBM-bound
+// (~0.4 flop/byte at 7 diagonals) and stay on the VALU; wide dense bands take
+// the f64 MFMA form k_dia_mfma (DIA).
 #include "ias.h"
 #include "ias_internal.hpp"
 #include "spgemm_engine.hpp"
@@ -19,6 +21,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace ias {
@@ -134,6 +138,9 @@ struct DiaMfmaArgs {
     const int32_t *amap, *bmap, *cmap;   // offset - lo -> diagonal slot or -1
     const double *va, *vb;
     double *vc;
+    const int32_t *offa, *offb;          // diagonal offsets (the VALU fallback)
+    const int32_t *tab;                  // pair table: start[ndc + 1], ja[np], kb[np]
+    int32_t np;
 };
 
 __global__ __launch_bounds__(256) void k_dia_mfma(DiaMfmaArgs a) {
@@ -148,18 +155,42 @@ __global__ __launch_bounds__(256) void k_dia_mfma(DiaMfmaArgs a) {
     int32_t *bm = am + a.span_a + 1;
     int32_t *cm = bm + a.span_b + 1;
     const int t = (int)threadIdx.x;
+    int bad = 0;   // a non-finite operand: 0 * Inf in the dense block would be NaN
     for (int i = t; i < 16 * a.nda; i += 256) {
         const int r = i / a.nda;
-        sA[i] = i0 + r < a.rows ? a.va[(int64_t)(i0 + r) * a.nda + (i - r * a.nda)] : 0.0;
+        const double v = i0 + r < a.rows ? a.va[(int64_t)(i0 + r) * a.nda + (i - r * a.nda)] : 0.0;
+        bad |= !__builtin_isfinite(v);
+        sA[i] = v;
     }
     for (int i = t; i < WA * a.ndb; i += 256) {
         const int r = i / a.ndb, br = cA0 + r;
-        sB[i] = (br >= 0 && br < a.a_cols) ? a.vb[(int64_t)br * a.ndb + (i - r * a.ndb)] : 0.0;
+        const double v = (br >= 0 && br < a.a_cols) ? a.vb[(int64_t)br * a.ndb + (i - r * a.ndb)] : 0.0;
+        bad |= !__builtin_isfinite(v);
+        sB[i] = v;
     }
     for (int i = t; i <= a.span_a; i += 256) am[i] = a.amap[i];
     for (int i = t; i <= a.span_b; i += 256) bm[i] = a.bmap[i];
     for (int i = t; i <= a.span_c; i += 256) cm[i] = a.cmap[i];
-    __syncthreads();
+    if (__syncthreads_or(bad)) {
+        // this tile holds an Inf / NaN: the reference's pair sums on the VALU
+        // (k_dia_tile's loop over the staged rows; bitwise the reference)
+        const int32_t *sja = a.tab + a.ndc + 1, *skb = sja + a.np;
+        for (int e = t; e < 16 * a.ndc; e += 256) {
+            const int i = e / a.ndc, slot = e - i * a.ndc, gi = i0 + i;
+            if (gi >= a.rows) break;
+            double acc = 0.0;
+            for (int p = a.tab[slot]; p < a.tab[slot + 1]; ++p) {
+                const int ja = sja[p], kb = skb[p];
+                const int acol = gi + a.offa[ja];
+                if (acol < 0 || acol >= a.a_cols) continue;
+                const int bcol = acol + a.offb[kb];
+                if (bcol < 0 || bcol >= a.b_cols) continue;
+                acc = acc + sA[i * a.nda + ja] * sB[(acol - cA0) * a.ndb + kb];
+            }
+            a.vc[(int64_t)gi * a.ndc + slot] = acc;
+        }
+        return;
+    }
     const int w = t >> 6, l = t & 63;
     const int nblk = (WC + 15) / 16;
     for (int cb = w; cb < nblk; cb += 4) {
@@ -260,6 +291,106 @@ static void dia_plan(const int32_t *offa, int32_t nda, const int32_t *offb, int3
         }                                                                         \
     } while (0)
 
+// Per offset set (A's and B's diagonal offsets and the shapes), everything
+// the call derives from the offsets alone: C's offsets, the pair table, the
+// MFMA offset maps, and their device copies — computed once and reused by
+// later calls (the K1 step is a 31 µs kernel: the host plan, three small
+// synchronous uploads and two event creations cost more than the kernel).
+namespace {
+struct DiaPlan {
+    std::vector<int32_t> offc, pst, pja, pkb, maps;
+    int32_t lo_a = 0, span_a = 0, lo_b = 0, span_b = 0, lo_c = 0, span_c = 0;
+    int64_t flops = 0;                // multiply pairs formed (in range)
+    int32_t *d_offc = nullptr, *d_tab = nullptr, *d_maps = nullptr;
+    int32_t *d_offa = nullptr, *d_offb = nullptr;
+};
+struct DiaCache {
+    std::mutex mu;
+    std::map<std::vector<int64_t>, DiaPlan *> plans;   // never freed: a plan is tiny
+};
+DiaCache &dia_cache() {
+    static DiaCache *c = new DiaCache;
+    return *c;
+}
+ias_status upload_i32(int32_t **d, const std::vector<int32_t> &h, int device) {
+    IAS_TRY(dev_alloc((void **)d, 4 * std::max<size_t>(h.size(), 1), device));
+    if (!h.empty()) IAS_TRY(dev_copy_h2d(*d, h.data(), 4 * h.size(), device));
+    return IAS_SUCCESS;
+}
+ias_status dia_plan_get(const std::vector<int32_t> &offa, const std::vector<int32_t> &offb, int64_t rows,
+                        int64_t a_cols, int64_t b_cols, int device, const DiaPlan **out) {
+    std::vector<int64_t> key{device, rows, a_cols, b_cols, (int64_t)offa.size()};
+    key.insert(key.end(), offa.begin(), offa.end());
+    key.insert(key.end(), offb.begin(), offb.end());
+    DiaCache &c = dia_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    auto it = c.plans.find(key);
+    if (it != c.plans.end()) {
+        *out = it->second;
+        return IAS_SUCCESS;
+    }
+    DiaPlan *P = new DiaPlan;
+    const int32_t nda = (int32_t)offa.size(), ndb = (int32_t)offb.size();
+    dia_plan(offa.data(), nda, offb.data(), ndb, rows, a_cols, b_cols, P->offc, P->pst, P->pja, P->pkb);
+    const int32_t ndc = (int32_t)P->offc.size();
+    if (nda && ndb && ndc) {
+        P->lo_a = *std::min_element(offa.begin(), offa.end());
+        P->span_a = *std::max_element(offa.begin(), offa.end()) - P->lo_a;
+        P->lo_b = *std::min_element(offb.begin(), offb.end());
+        P->span_b = *std::max_element(offb.begin(), offb.end()) - P->lo_b;
+        P->lo_c = P->offc.front();
+        P->span_c = P->offc.back() - P->lo_c;
+        // offset -> slot maps of the MFMA operands, only for bands narrow
+        // enough for its LDS (a wide-offset band never takes that kernel)
+        const int64_t mlen = (int64_t)P->span_a + P->span_b + P->span_c + 3;
+        if (mlen <= (1 << 16)) {
+            P->maps.assign((size_t)mlen, -1);
+            for (int32_t j = 0; j < nda; ++j) P->maps[offa[j] - P->lo_a] = j;
+            for (int32_t j = 0; j < ndb; ++j) P->maps[(size_t)P->span_a + 1 + (offb[j] - P->lo_b)] = j;
+            for (int32_t j = 0; j < ndc; ++j)
+                P->maps[(size_t)P->span_a + P->span_b + 2 + (P->offc[j] - P->lo_c)] = j;
+        }
+    }
+    for (int32_t d = 0; d < ndc; ++d)
+        for (int32_t q = P->pst[d]; q < P->pst[d + 1]; ++q) {
+            const int64_t oa = offa[P->pja[q]], ob = offb[P->pkb[q]];
+            const int64_t lo = std::max<int64_t>(0, std::max<int64_t>(-oa, -oa - ob));
+            const int64_t hi = std::min<int64_t>(rows, std::min<int64_t>(a_cols - oa, b_cols - oa - ob));
+            if (hi > lo) P->flops += hi - lo;
+        }
+    std::vector<int32_t> tab;
+    tab.insert(tab.end(), P->pst.begin(), P->pst.end());
+    tab.insert(tab.end(), P->pja.begin(), P->pja.end());
+    tab.insert(tab.end(), P->pkb.begin(), P->pkb.end());
+    ias_status st;
+    if ((st = upload_i32(&P->d_offc, P->offc, device)) || (st = upload_i32(&P->d_tab, tab, device)) ||
+        (st = upload_i32(&P->d_maps, P->maps, device)) || (st = upload_i32(&P->d_offa, offa, device)) ||
+        (st = upload_i32(&P->d_offb, offb, device))) {
+        for (int32_t *q : {P->d_offc, P->d_tab, P->d_maps, P->d_offa, P->d_offb}) dev_free(q, device);
+        delete P;
+        return st;
+    }
+    if (c.plans.size() < 256) c.plans[key] = P;   // beyond that: planned per call (leaked, tiny)
+    *out = P;
+    return IAS_SUCCESS;
+}
+// two timing events per (thread, device), created once
+void dia_events(int device, hipEvent_t *e0, hipEvent_t *e1) {
+    thread_local std::map<int, std::pair<hipEvent_t, hipEvent_t>> evs;
+    auto it = evs.find(device);
+    if (it == evs.end()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+            *e0 = *e1 = nullptr;
+            return;
+        }
+        it = evs.emplace(device, std::make_pair(a, b)).first;
+    }
+    *e0 = it->second.first;
+    *e1 = it->second.second;
+}
+}  // namespace
+
 extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
                                       const ias_opts *opts, ias_report *rep) {
     if (!A || !B || !C) return IAS_ERROR_INVALID_ARGUMENT;
@@ -275,20 +406,18 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
 
     // offsets on the host (tiny)
     std::vector<int32_t> offa(A->num_diagonals), offb(B->num_diagonals);
-    if (A->num_diagonals) {
-        if (A->memory == IAS_MEMORY_DEVICE)
-            IAS_TRY(dev_copy_d2h(offa.data(), A->diagonal_offsets, 4 * offa.size(), A->device));
-        else memcpy(offa.data(), A->diagonal_offsets, 4 * offa.size());
-    }
-    if (B->num_diagonals) {
-        if (B->memory == IAS_MEMORY_DEVICE)
-            IAS_TRY(dev_copy_d2h(offb.data(), B->diagonal_offsets, 4 * offb.size(), B->device));
-        else memcpy(offb.data(), B->diagonal_offsets, 4 * offb.size());
-    }
-    std::vector<int32_t> offc, pst, pja, pkb;
-    dia_plan(offa.data(), A->num_diagonals, offb.data(), B->num_diagonals, A->rows, A->cols,
-             B->cols, offc, pst, pja, pkb);
-    const int32_t ndc = (int32_t)offc.size();
+    auto read_offsets = [&](const ias_dia *X, std::vector<int32_t> &h) -> ias_status {
+        if (h.empty()) return IAS_SUCCESS;
+        if (X->memory == IAS_MEMORY_DEVICE) return dev_copy_d2h(h.data(), X->diagonal_offsets, 4 * h.size(), X->device);
+        memcpy(h.data(), X->diagonal_offsets, 4 * h.size());
+        return IAS_SUCCESS;
+    };
+    IAS_TRY(read_offsets(A, offa));
+    if (B == A) offb = offa;
+    else IAS_TRY(read_offsets(B, offb));
+    const DiaPlan *P = nullptr;
+    IAS_TRY(dia_plan_get(offa, offb, A->rows, A->cols, B->cols, device, &P));
+    const int32_t ndc = (int32_t)P->offc.size();
 
     hipStream_t s = (hipStream_t)o.stream;
     bool own = false;
@@ -297,13 +426,18 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
         HIPC(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         own = true;
     }
+    // Everything this call allocates is released on every exit path (after
+    // its stream has drained): staging copies, and D unless handed to C.
     struct Cleanup {
         std::vector<void *> p;
         int dev;
         hipStream_t s;
         bool own;
+        ias_dia *D = nullptr;
         ~Cleanup() {
+            hipStreamSynchronize(s);
             for (void *x : p) dev_free(x, dev);
+            if (D) ias_dia_free(D);
             if (own) hipStreamDestroy(s);
         }
     } cl{{}, device, s, own};
@@ -322,24 +456,11 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
         *out = d;
         return IAS_SUCCESS;
     };
-    const void *da_off, *da_val, *db_off, *db_val;
+    const void *da_val, *db_val;
     const size_t na = (size_t)A->rows * A->num_diagonals, nb = (size_t)B->rows * B->num_diagonals;
-    IAS_TRY(stage(A->diagonal_offsets, 4 * offa.size(), A->memory, A->device, &da_off));
     IAS_TRY(stage(A->val, 8 * na, A->memory, A->device, &da_val));
-    if (B == A) {
-        db_off = da_off;
-        db_val = da_val;
-    } else {
-        IAS_TRY(stage(B->diagonal_offsets, 4 * offb.size(), B->memory, B->device, &db_off));
-        IAS_TRY(stage(B->val, 8 * nb, B->memory, B->device, &db_val));
-    }
-    // pair tables (host -> device, a few hundred bytes)
-    std::vector<int32_t> tab;
-    tab.insert(tab.end(), pst.begin(), pst.end());
-    tab.insert(tab.end(), pja.begin(), pja.end());
-    tab.insert(tab.end(), pkb.begin(), pkb.end());
-    const void *dtab;
-    IAS_TRY(stage(tab.data(), 4 * tab.size(), IAS_MEMORY_HOST, 0, &dtab));
+    if (B == A) db_val = da_val;
+    else IAS_TRY(stage(B->val, 8 * nb, B->memory, B->device, &db_val));
 
     ias_dia D{};
     D.rows = A->rows;
@@ -348,110 +469,88 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     D.choice = 1;
     D.memory = IAS_MEMORY_DEVICE;
     D.device = device;
+    cl.D = &D;
     const int64_t span = std::max<int64_t>(A->rows + B->cols - 1, 0);
-    void *p0 = nullptr, *p1 = nullptr, *p2 = nullptr;
-    ias_status sa;
-    if ((sa = dev_alloc(&p0, 4 * (size_t)ndc, device)) || (sa = dev_alloc(&p1, 4 * (size_t)span, device)) ||
-        (sa = dev_alloc(&p2, 8 * (size_t)A->rows * ndc, device))) {
-        D.diagonal_offsets = (int32_t *)p0; D.diagonal_ind = (int32_t *)p1; D.val = (double *)p2;
-        ias_dia_free(&D);
-        return sa;
-    }
-    D.diagonal_offsets = (int32_t *)p0; D.diagonal_ind = (int32_t *)p1; D.val = (double *)p2;
-    HIPC(hipMemcpyAsync(D.diagonal_offsets, offc.data(), 4 * (size_t)ndc, hipMemcpyHostToDevice, s));
-    HIPC(hipMemsetAsync(D.diagonal_ind, 0, 4 * (size_t)span, s));
+    IAS_TRY(dev_alloc((void **)&D.diagonal_offsets, 4 * (size_t)ndc, device));
+    IAS_TRY(dev_alloc((void **)&D.diagonal_ind, 4 * (size_t)span, device));
+    IAS_TRY(dev_alloc((void **)&D.val, 8 * (size_t)A->rows * ndc, device));
+    if (ndc) HIPC(hipMemcpyAsync(D.diagonal_offsets, P->d_offc, 4 * (size_t)ndc, hipMemcpyDeviceToDevice, s));
+    if (span) HIPC(hipMemsetAsync(D.diagonal_ind, 0, 4 * (size_t)span, s));
 
-    hipEvent_t e0, e1;
-    HIPC(hipEventCreate(&e0));
-    HIPC(hipEventCreate(&e1));
-    HIPC(hipEventRecord(e0, s));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (rep) dia_events(device, &e0, &e1);
+    if (e0) HIPC(hipEventRecord(e0, s));
     const int64_t n = A->rows * (int64_t)ndc;
-    const int32_t nda = A->num_diagonals, ndb = B->num_diagonals, np = (int32_t)pja.size();
+    const int32_t nda = A->num_diagonals, ndb = B->num_diagonals, np = (int32_t)P->pja.size();
     if (ndc > 0) {
         dev::k_dia_index<<<(ndc + 255) / 256, 256, 0, s>>>(ndc, D.diagonal_offsets, A->rows, D.diagonal_ind);
         if (n > 0) {
-            const int32_t *t = (const int32_t *)dtab;
-            const int32_t lo_a = *std::min_element(offa.begin(), offa.end());
-            const int32_t span_a = *std::max_element(offa.begin(), offa.end()) - lo_a;
-            const int32_t lo_b = *std::min_element(offb.begin(), offb.end());
-            const int32_t span_b = *std::max_element(offb.begin(), offb.end()) - lo_b;
+            const int32_t *t = P->d_tab;
+            const int32_t lo_a = P->lo_a, span_a = P->span_a, lo_b = P->lo_b, span_b = P->span_b;
             const bool small = A->rows < (1ll << 30) && A->cols < (1ll << 30) && B->cols < (1ll << 30);
-            const char *mf = getenv("IAS_DIA_MFMA");
             int32_t tr = 64;
             auto tile_lds = [&](int32_t r) {
                 return 8ull * ((uint64_t)r * nda + (uint64_t)(r + span_a) * ndb) + 4ull * (nda + ndb + ndc + 1 + 2 * np);
             };
             while (tile_lds(tr) > 65536 && tr > 16) tr /= 2;
-            // MFMA for wide bands (measured: 65 diagonals, K1w, 0.57 ms vs 5.5 ms
-            // for the tiled VALU kernel; 7 diagonals, K1, 54 vs 32 us), VALU
-            // (bitwise the reference) otherwise; IAS_DIA_MFMA=0/1 forces either
-            const bool use_mfma = mf ? *mf == '1' : (int64_t)nda * ndb >= 256;
-            if (use_mfma && small) {
-                // offset -> slot maps for the dense-block operands
-                const int32_t lo_c = offc.front(), span_c = offc.back() - lo_c;
-                std::vector<int32_t> maps((size_t)span_a + span_b + span_c + 3, -1);
-                for (int32_t j = 0; j < nda; ++j) maps[offa[j] - lo_a] = j;
-                for (int32_t j = 0; j < ndb; ++j) maps[(size_t)span_a + 1 + (offb[j] - lo_b)] = j;
-                for (int32_t j = 0; j < ndc; ++j) maps[(size_t)span_a + span_b + 2 + (offc[j] - lo_c)] = j;
-                const void *dmaps;
-                IAS_TRY(stage(maps.data(), 4 * maps.size(), IAS_MEMORY_HOST, 0, &dmaps));
-                const int32_t *m = (const int32_t *)dmaps;
-                const int32_t WA = 16 + span_a;
-                const size_t lds = 8ull * (16ull * nda + (uint64_t)WA * ndb) + 4ull * maps.size();
-                if (lds > 160 * 1024) return IAS_ERROR_INVALID_ARGUMENT;
-                if (lds > 65536)
-                    hipFuncSetAttribute((const void *)dev::k_dia_mfma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024);
+            // MFMA for wide DENSE bands (measured: 65 contiguous diagonals, K1w,
+            // 0.57 ms vs 5.5 ms for the tiled VALU kernel; 7 diagonals, K1, 54
+            // vs 32 us): at least 256 diagonal pairs, and the 16-row tile's
+            // dense blocks (16 x W_A x W_C products) at most 4x the band's
+            // products (16 x nd_A x nd_B) — a band of widely spaced diagonals
+            // (a 27-point stencil at offsets of +-n^2) would be almost all
+            // padding — and its operands within one CU's LDS.  IAS_DIA_MFMA=0/1
+            // forces either where the MFMA form is possible at all.
+            const int64_t WA = 16 + (int64_t)span_a, WC = WA + span_b;
+            const size_t mfma_lds = 8ull * (16ull * nda + (uint64_t)WA * ndb) + 4ull * P->maps.size();
+            const bool mfma_ok = small && !P->maps.empty() && mfma_lds <= 160 * 1024;
+            const char *mf = getenv("IAS_DIA_MFMA");
+            const bool dense = (int64_t)nda * ndb >= 256 && WA * WC <= 4ll * nda * ndb;
+            const bool use_mfma = mfma_ok && (mf ? *mf == '1' : dense);
+            if (use_mfma) {
+                const int32_t *m = P->d_maps;
+                if (mfma_lds > 65536)
+                    HIPC(hipFuncSetAttribute((const void *)dev::k_dia_mfma,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
                 HIPC(hipMemsetAsync(D.val, 0, 8 * (size_t)n, s));
                 dev::DiaMfmaArgs ma{(int32_t)A->rows, (int32_t)A->cols, (int32_t)B->cols, nda, ndb, ndc,
-                                    lo_a, span_a, lo_b, span_b, lo_c, span_c,
+                                    lo_a, span_a, lo_b, span_b, P->lo_c, P->span_c,
                                     m, m + span_a + 1, m + span_a + span_b + 2,
-                                    (const double *)da_val, (const double *)db_val, D.val};
-                dev::k_dia_mfma<<<(unsigned)((A->rows + 15) / 16), 256, lds, s>>>(ma);
+                                    (const double *)da_val, (const double *)db_val, D.val,
+                                    P->d_offa, P->d_offb, t, np};
+                dev::k_dia_mfma<<<(unsigned)((A->rows + 15) / 16), 256, mfma_lds, s>>>(ma);
             } else if (small && tile_lds(tr) <= 65536) {
                 const uint64_t magic = ((1ull << 32) + (uint64_t)ndc - 1) / (uint64_t)ndc;
                 dev::DiaTileArgs ta{(int32_t)A->rows, (int32_t)A->cols, (int32_t)B->cols, nda, ndb, ndc, np,
-                                    lo_a, span_a, tr, magic, (const int32_t *)da_off, (const int32_t *)db_off,
+                                    lo_a, span_a, tr, magic, P->d_offa, P->d_offb,
                                     (const double *)da_val, (const double *)db_val, t, D.val};
                 dev::k_dia_tile<<<(unsigned)((A->rows + tr - 1) / tr), 256, tile_lds(tr), s>>>(ta);
             } else {
-                dev::DiaPairs pr{t, t + pst.size(), t + pst.size() + pja.size()};
+                dev::DiaPairs pr{t, t + P->pst.size(), t + P->pst.size() + P->pja.size()};
                 dev::k_dia_mul<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(
-                    A->rows, A->cols, B->cols, A->num_diagonals, (const int32_t *)da_off,
-                    (const double *)da_val, B->num_diagonals, (const int32_t *)db_off,
+                    A->rows, A->cols, B->cols, nda, P->d_offa, (const double *)da_val, ndb, P->d_offb,
                     (const double *)db_val, ndc, pr, D.val);
             }
         }
     }
     HIPC(hipGetLastError());
-    HIPC(hipEventRecord(e1, s));
+    if (e1) HIPC(hipEventRecord(e1, s));
     HIPC(hipStreamSynchronize(s));
     if (rep) {
         float t = 0;
-        hipEventElapsedTime(&t, e0, e1);
+        if (e0 && e1) hipEventElapsedTime(&t, e0, e1);
         rep->ms_total = t;
         rep->ms_numeric = t;
-        int64_t fl = 0;   // multiply pairs actually formed (in-range)
-        for (int32_t d = 0; d < ndc; ++d)
-            for (int32_t p = pst[d]; p < pst[d + 1]; ++p) {
-                const int64_t oa = offa[pja[p]], ob = offb[pkb[p]];
-                int64_t lo = std::max<int64_t>(0, std::max<int64_t>(-oa, -oa - ob));
-                int64_t hi = std::min<int64_t>(A->rows, std::min<int64_t>(A->cols - oa, B->cols - oa - ob));
-                if (hi > lo) fl += hi - lo;
-            }
-        rep->flops = fl;
+        rep->flops = P->flops;
         rep->nnz_c = n;
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
     if (out_mem == IAS_MEMORY_HOST) {
         ias_dia H{};
-        ias_status cs = ias_dia_copy(&D, &H, IAS_MEMORY_HOST, 0);
-        ias_dia_free(&D);
-        if (cs != IAS_SUCCESS) return cs;
-        *C = H;
+        IAS_TRY(ias_dia_copy(&D, &H, IAS_MEMORY_HOST, 0));
+        *C = H;   // D is freed by the cleanup
     } else {
         *C = D;
+        cl.D = nullptr;
     }
     return IAS_SUCCESS;
 }

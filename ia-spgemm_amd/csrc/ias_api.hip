@@ -45,11 +45,14 @@ void host_free(void *p) { free(p); }
 // Device blocks of the library-allocated outputs and staging copies go
 // through a small per-device cache: blocks up to 256 MiB are rounded to a
 // power of two and kept on free (up to 1 GiB per device) instead of
-// hipFree'd — hipFree synchronises the device and hipMalloc costs tens of µs,
-// which dominated calls on small operands (K1 through the DIA kernel: 0.43 ms
-// per call around a 32 µs kernel).  A freed block is reused only by a later
-// call on the same device; every call synchronises its stream before it
-// returns, so no kernel still uses a block handed back here.
+// hipFree'd — hipFree costs hundreds of µs (it synchronises the device and
+// unmaps), which dominated calls on small operands (K1 through the DIA kernel:
+// 0.43 ms per call around a 32 µs kernel).  Returning a block to the cache
+// keeps hipFree's ordering guarantee: the device is synchronised first (a few
+// µs when idle), so no kernel of any stream — an error path's side streams, a
+// caller's own work on a library-allocated output — still reads or writes a
+// block a later call may be handed.  When hipMalloc runs out of memory the
+// device's cached free blocks are released and the allocation retried once.
 namespace {
 struct BlockCache {
     static constexpr size_t MAX_BLOCK = 256ull << 20, MAX_TOTAL = 1ull << 30;
@@ -61,6 +64,26 @@ struct BlockCache {
         size_t r = 256;
         while (r < b) r <<= 1;
         return r;
+    }
+    // hipFree every cached free block of `device` (caller holds no lock)
+    void trim(int device) {
+        std::vector<void *> drop;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            for (auto it = free.begin(); it != free.end();) {
+                if (it->first.first == device) {
+                    for (void *q : it->second) {
+                        drop.push_back(q);
+                        size_of.erase(q);
+                    }
+                    held[device] -= it->first.second * it->second.size();
+                    it = free.erase(it);
+                } else {
+                    ++it;
+                }
+            }
+        }
+        for (void *q : drop) hipFree(q);
     }
 };
 BlockCache &cache() {
@@ -74,43 +97,54 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
     HIPC(hipSetDevice(device));
     if (bytes == 0) bytes = 8;
     BlockCache &c = cache();
-    if (bytes <= BlockCache::MAX_BLOCK && device >= 0 && device < 64) {
-        const size_t r = BlockCache::round(bytes);
-        {
-            std::lock_guard<std::mutex> g(c.mu);
-            auto it = c.free.find({device, r});
-            if (it != c.free.end() && !it->second.empty()) {
-                *p = it->second.back();
-                it->second.pop_back();
-                c.held[device] -= r;
-                return IAS_SUCCESS;
-            }
-        }
-        HIPC(hipMalloc(p, r));
+    const bool cached = bytes <= BlockCache::MAX_BLOCK && device >= 0 && device < 64;
+    const size_t want = cached ? BlockCache::round(bytes) : bytes;
+    if (cached) {
         std::lock_guard<std::mutex> g(c.mu);
-        c.size_of[*p] = r;
-        return IAS_SUCCESS;
+        auto it = c.free.find({device, want});
+        if (it != c.free.end() && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            c.held[device] -= want;
+            return IAS_SUCCESS;
+        }
     }
-    HIPC(hipMalloc(p, bytes));
+    hipError_t e = hipMalloc(p, want);
+    if (e == hipErrorOutOfMemory && device >= 0 && device < 64) {
+        (void)hipGetLastError();
+        c.trim(device);
+        e = hipMalloc(p, want);
+    }
+    HIPC(e);
+    if (cached) {
+        std::lock_guard<std::mutex> g(c.mu);
+        c.size_of[*p] = want;
+    }
     return IAS_SUCCESS;
 }
 ias_status dev_free(void *p, int device) {
     if (!p) return IAS_SUCCESS;
     BlockCache &c = cache();
+    bool keep = false;
     {
         std::lock_guard<std::mutex> g(c.mu);
         auto it = c.size_of.find(p);
         if (it != c.size_of.end() && device >= 0 && device < 64) {
-            const size_t r = it->second;
-            if (c.held[device] + r <= BlockCache::MAX_TOTAL) {
-                c.free[{device, r}].push_back(p);
-                c.held[device] += r;
-                return IAS_SUCCESS;
-            }
-            c.size_of.erase(it);
+            if (c.held[device] + it->second <= BlockCache::MAX_TOTAL) keep = true;
+            else c.size_of.erase(it);
         }
     }
     HIPC(hipSetDevice(device));
+    if (keep) {
+        // hipFree's ordering: nothing still running may touch the block once
+        // a later call can be handed it
+        HIPC(hipDeviceSynchronize());
+        std::lock_guard<std::mutex> g(c.mu);
+        const size_t r = c.size_of[p];
+        c.free[{device, r}].push_back(p);
+        c.held[device] += r;
+        return IAS_SUCCESS;
+    }
     HIPC(hipFree(p));
     return IAS_SUCCESS;
 }

@@ -26,6 +26,10 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <string>
 #include <cstring>
 #include <mutex>
 #include <thread>
@@ -195,10 +199,150 @@ __global__ void k_shift_ends(const int64_t *rp, int64_t rows, int64_t off, int64
     if (i < rows) out[i] = rp[i + 1] - rp[0] + off;
 }
 
+// The exchange step's two collectives, behind one interface:
+// RCCL for one process per GPU, and a loopback (in-process, memcpy) form for
+// P ranks driven by P host threads of one process — on one GPU or several —
+// so the sharding, the per-root offsets and the row-pointer fix-up run at
+// P > 1 where RCCL cannot (it allows one rank per device in a communicator).
+struct Bcast {
+    const void *send;   // the root's source (others: ignored)
+    void *recv;
+    size_t bytes;
+    int root;
+};
+struct Transport {
+    virtual ~Transport() {}
+    // recv[r * n .. r * n + n) = rank r's send[0 .. n), device buffers
+    virtual ias_status allgather_i64(const int64_t *send, int64_t *recv, size_t n, hipStream_t s) = 0;
+    // every op of the list as one group (the same list on every rank)
+    virtual ias_status bcast_group(const std::vector<Bcast> &ops, hipStream_t s) = 0;
+};
+
+struct RcclTransport : Transport {
+    const Rccl *R;
+    ncclComm_t comm;
+    RcclTransport(const Rccl *r, ncclComm_t c) : R(r), comm(c) {}
+    ~RcclTransport() override {
+        if (comm) R->CommDestroy(comm);
+    }
+    ias_status allgather_i64(const int64_t *send, int64_t *recv, size_t n, hipStream_t s) override {
+        RCCL_TRY(R->AllGather(send, recv, n, ncclInt64, comm, s));
+        return IAS_SUCCESS;
+    }
+    ias_status bcast_group(const std::vector<Bcast> &ops, hipStream_t s) override {
+        RCCL_TRY(R->GroupStart());
+        for (const Bcast &b : ops) {
+            // 8-byte elements where the size allows (the C arrays), bytes otherwise
+            const bool w8 = b.bytes % 8 == 0;
+            const ncclResult_t rc = R->Broadcast(b.send, b.recv, w8 ? b.bytes / 8 : b.bytes, w8 ? ncclInt64 : ncclInt8,
+                                                 b.root, comm, s);
+            if (rc != ncclSuccess) {
+                R->GroupEnd();
+                set_last_error("ncclBroadcast: %s", R->GetErrorString ? R->GetErrorString(rc) : "rccl error");
+                return IAS_ERROR_DEVICE;
+            }
+        }
+        RCCL_TRY(R->GroupEnd());
+        return IAS_SUCCESS;
+    }
+};
+
+// Loopback group: P ranks of one process meet at a host barrier; every rank
+// posts its (already complete: its stream is synchronised first) send
+// buffers, copies what it receives from the peers' buffers with
+// hipMemcpyAsync on its own stream, drains it, and meets the others again
+// before returning (no peer buffer is released while still being read).
+struct LoopGroup {
+    int P;
+    std::mutex mu;
+    std::condition_variable cv;
+    int waiting = 0;
+    uint64_t gen = 0;
+    std::vector<const void *> posted;                 // allgather: per rank
+    std::vector<std::vector<Bcast>> posted_ops;       // bcast: per rank
+    explicit LoopGroup(int p) : P(p), posted(p), posted_ops(p) {}
+    bool broken = false;   // a rank gave up waiting: the group is unusable
+    // false when the peers did not all arrive within `secs` (a rank failed
+    // before reaching the collective): every rank then returns an error
+    // instead of waiting forever
+    bool barrier(double secs = 300.0) {
+        std::unique_lock<std::mutex> g(mu);
+        if (broken) return false;
+        const uint64_t my = gen;
+        if (++waiting == P) {
+            waiting = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        const bool ok = cv.wait_for(g, std::chrono::duration<double>(secs), [&] { return gen != my || broken; });
+        if (!ok || broken) {
+            broken = true;
+            cv.notify_all();
+            return false;
+        }
+        return true;
+    }
+};
+std::mutex &loop_registry_mu() {
+    static std::mutex *m = new std::mutex;
+    return *m;
+}
+std::map<std::string, std::weak_ptr<LoopGroup>> &loop_registry() {
+    static auto *m = new std::map<std::string, std::weak_ptr<LoopGroup>>;
+    return *m;
+}
+
+struct LoopTransport : Transport {
+    std::shared_ptr<LoopGroup> g;
+    int rank;
+    LoopTransport(std::shared_ptr<LoopGroup> grp, int r) : g(std::move(grp)), rank(r) {}
+    static ias_status lost() {
+        set_last_error("loopback group: a peer rank did not reach the collective");
+        return IAS_ERROR_DEVICE;
+    }
+    ias_status allgather_i64(const int64_t *send, int64_t *recv, size_t n, hipStream_t s) override {
+        HIPC(hipStreamSynchronize(s));
+        g->posted[rank] = send;
+        if (!g->barrier()) return lost();
+        hipError_t e = hipSuccess;
+        for (int r = 0; r < g->P && e == hipSuccess; ++r)
+            e = hipMemcpyAsync(recv + (size_t)r * n, g->posted[r], n * sizeof(int64_t), hipMemcpyDefault, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        const bool met = g->barrier();   // every peer done reading this rank's buffer (also on error)
+        HIPC(e);
+        return met ? IAS_SUCCESS : lost();
+    }
+    ias_status bcast_group(const std::vector<Bcast> &ops, hipStream_t s) override {
+        HIPC(hipStreamSynchronize(s));
+        g->posted_ops[rank] = ops;
+        if (!g->barrier()) return lost();
+        hipError_t e = hipSuccess;
+        for (size_t k = 0; k < ops.size() && e == hipSuccess; ++k) {
+            const auto &root_ops = g->posted_ops[ops[k].root];
+            const void *src = k < root_ops.size() ? root_ops[k].send : nullptr;
+            if (!src) {
+                e = hipErrorInvalidValue;
+                break;
+            }
+            if (src != ops[k].recv && ops[k].bytes)
+                e = hipMemcpyAsync(ops[k].recv, src, ops[k].bytes, hipMemcpyDefault, s);
+        }
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        const bool met = g->barrier();
+        if (!met) return lost();
+        if (e != hipSuccess) {
+            set_last_error("loopback broadcast: %s", hipGetErrorString(e));
+            return IAS_ERROR_DEVICE;
+        }
+        return IAS_SUCCESS;
+    }
+};
+
 }  // namespace
 
 struct ias_dist {
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Transport> tr;
     int rank = 0, nranks = 1, device = 0;
     ias_plan *plan = nullptr;
 };
@@ -213,26 +357,9 @@ extern "C" ias_status ias_dist_unique_id(char *id, int32_t id_len) {
     return IAS_SUCCESS;
 }
 
-extern "C" ias_status ias_dist_create(ias_dist **out, const char *id, int32_t nranks, int32_t rank, int32_t device) {
-    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return IAS_ERROR_INVALID_ARGUMENT;
-    const Rccl *R = rccl();
-    if (!R) return IAS_ERROR_DEVICE;
-    HIPC(hipSetDevice(device));
-    ncclUniqueId u;
-    memcpy(&u, id, sizeof u);
-    ias_dist *d = new ias_dist;
-    d->rank = rank;
-    d->nranks = nranks;
-    d->device = device;
-    const ncclResult_t rc = R->CommInitRank(&d->comm, nranks, u, rank);
-    if (rc != ncclSuccess) {
-        set_last_error("ncclCommInitRank: %s", R->GetErrorString ? R->GetErrorString(rc) : "rccl error");
-        delete d;
-        return IAS_ERROR_DEVICE;
-    }
+static ias_status dist_finish(ias_dist *d, int32_t device, ias_dist **out) {
     const ias_status s = ias_plan_create(&d->plan, device, nullptr);
     if (s != IAS_SUCCESS) {
-        R->CommDestroy(d->comm);
         delete d;
         return s;
     }
@@ -240,11 +367,57 @@ extern "C" ias_status ias_dist_create(ias_dist **out, const char *id, int32_t nr
     return IAS_SUCCESS;
 }
 
+extern "C" ias_status ias_dist_create(ias_dist **out, const char *id, int32_t nranks, int32_t rank, int32_t device) {
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks) return IAS_ERROR_INVALID_ARGUMENT;
+    const Rccl *R = rccl();
+    if (!R) return IAS_ERROR_DEVICE;
+    HIPC(hipSetDevice(device));
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t rc = R->CommInitRank(&comm, nranks, u, rank);
+    if (rc != ncclSuccess) {
+        set_last_error("ncclCommInitRank: %s", R->GetErrorString ? R->GetErrorString(rc) : "rccl error");
+        return IAS_ERROR_DEVICE;
+    }
+    ias_dist *d = new ias_dist;
+    d->tr.reset(new RcclTransport(R, comm));
+    d->rank = rank;
+    d->nranks = nranks;
+    d->device = device;
+    return dist_finish(d, device, out);
+}
+
+extern "C" ias_status ias_dist_create_loopback(ias_dist **out, const char *group, int32_t nranks, int32_t rank,
+                                               int32_t device) {
+    if (!out || !group || nranks < 1 || rank < 0 || rank >= nranks) return IAS_ERROR_INVALID_ARGUMENT;
+    HIPC(hipSetDevice(device));
+    std::shared_ptr<LoopGroup> g;
+    {
+        std::lock_guard<std::mutex> lk(loop_registry_mu());
+        auto &reg = loop_registry();
+        auto it = reg.find(group);
+        if (it != reg.end()) g = it->second.lock();
+        if (g && g->P != nranks) {
+            set_last_error("loopback group '%s' has %d ranks, not %d", group, g->P, nranks);
+            return IAS_ERROR_INVALID_ARGUMENT;
+        }
+        if (!g) {
+            g = std::make_shared<LoopGroup>(nranks);
+            reg[group] = g;
+        }
+    }
+    ias_dist *d = new ias_dist;
+    d->tr.reset(new LoopTransport(g, rank));
+    d->rank = rank;
+    d->nranks = nranks;
+    d->device = device;
+    return dist_finish(d, device, out);
+}
+
 extern "C" ias_status ias_dist_destroy(ias_dist *d) {
     if (!d) return IAS_SUCCESS;
-    const Rccl *R = rccl();
     if (d->plan) ias_plan_destroy(d->plan);
-    if (R && d->comm) R->CommDestroy(d->comm);
     delete d;
     return IAS_SUCCESS;
 }
@@ -252,22 +425,32 @@ extern "C" ias_status ias_dist_destroy(ias_dist *d) {
 extern "C" ias_status ias_dist_allgatherv_csr(ias_dist *d, const ias_csr *Cl, ias_csr *Cf, void *stream) {
     if (!d || !Cl || !Cf) return IAS_ERROR_INVALID_ARGUMENT;
     if (Cl->memory != IAS_MEMORY_DEVICE || Cl->device != d->device) return IAS_ERROR_INVALID_ARGUMENT;
-    const Rccl *R = rccl();
-    if (!R) return IAS_ERROR_DEVICE;
     HIPC(hipSetDevice(d->device));
     hipStream_t s = (hipStream_t)stream;
     const int P = d->nranks;
+    // C_local may be a row view: its entries start at row_ptr[0]
+    int64_t rp0 = 0;
+    if (Cl->rows > 0) IAS_TRY(dev_copy_d2h(&rp0, Cl->row_ptr, sizeof(int64_t), d->device));
     // per-rank (rows, nnz)
-    int64_t *cnt = nullptr;
-    HIPC(hipMalloc(&cnt, sizeof(int64_t) * 2 * (P + 1)));
     std::vector<int64_t> h(2 * (P + 1));
-    h[0] = Cl->rows;
-    h[1] = Cl->nnz;
-    HIPC(hipMemcpyAsync(cnt + 2 * P, h.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, s));
-    RCCL_TRY(R->AllGather(cnt + 2 * P, cnt, 2, ncclInt64, d->comm, s));
-    HIPC(hipMemcpyAsync(h.data(), cnt, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    hipFree(cnt);
+    {
+        void *cntv = nullptr;
+        IAS_TRY(dev_alloc(&cntv, sizeof(int64_t) * 2 * (P + 1), d->device));
+        int64_t *cnt = (int64_t *)cntv;
+        h[0] = Cl->rows;
+        h[1] = Cl->nnz;
+        hipError_t e = hipMemcpyAsync(cnt + 2 * P, h.data(), 2 * sizeof(int64_t), hipMemcpyHostToDevice, s);
+        ias_status st = e == hipSuccess ? d->tr->allgather_i64(cnt + 2 * P, cnt, 2, s) : IAS_ERROR_DEVICE;
+        if (st == IAS_SUCCESS) {
+            e = hipMemcpyAsync(h.data(), cnt, sizeof(int64_t) * 2 * P, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) st = IAS_ERROR_DEVICE;
+        }
+        if (e != hipSuccess) set_last_error("allgatherv counts: %s", hipGetErrorString(e));
+        hipStreamSynchronize(s);
+        dev_free(cnt, d->device);
+        IAS_TRY(st);
+    }
     std::vector<int64_t> roff(P + 1, 0), noff(P + 1, 0);
     for (int r = 0; r < P; ++r) {
         roff[r + 1] = roff[r] + h[2 * r];
@@ -275,29 +458,46 @@ extern "C" ias_status ias_dist_allgatherv_csr(ias_dist *d, const ias_csr *Cl, ia
     }
     ias_csr F{};
     IAS_TRY(ias_csr_alloc(&F, roff[P], Cl->cols, noff[P], IAS_MEMORY_DEVICE, d->device));
-    HIPC(hipMemsetAsync(F.row_ptr, 0, sizeof(int64_t), s));
+    struct Guard {
+        ias_csr *F;
+        hipStream_t s;
+        ~Guard() {
+            if (F) {
+                hipStreamSynchronize(s);
+                ias_csr_free(F);
+            }
+        }
+    } guard{&F, s};
+    auto hipc = [](hipError_t e) -> ias_status {
+        if (e == hipSuccess) return IAS_SUCCESS;
+        set_last_error("allgatherv: %s", hipGetErrorString(e));
+        return e == hipErrorOutOfMemory ? IAS_ERROR_OUT_OF_MEMORY : IAS_ERROR_DEVICE;
+    };
+    IAS_TRY(hipc(hipMemsetAsync(F.row_ptr, 0, sizeof(int64_t), s)));
     // this rank's row ends, shifted into the global numbering, land in place
     if (Cl->rows > 0)
         k_shift_ends<<<(unsigned)((Cl->rows + 255) / 256), 256, 0, s>>>(Cl->row_ptr, Cl->rows, noff[d->rank],
                                                                         F.row_ptr + 1 + roff[d->rank]);
-    HIPC(hipGetLastError());
-    RCCL_TRY(R->GroupStart());
+    IAS_TRY(hipc(hipGetLastError()));
+    std::vector<Bcast> ops;
     for (int r = 0; r < P; ++r) {
         const bool me = r == d->rank;
         const int64_t rows = h[2 * r], nnz = h[2 * r + 1];
-        if (rows > 0)
-            RCCL_TRY(R->Broadcast(F.row_ptr + 1 + roff[r], F.row_ptr + 1 + roff[r], (size_t)rows, ncclInt64, r,
-                                  d->comm, s));
+        if (rows > 0) {
+            int64_t *slot = F.row_ptr + 1 + roff[r];
+            ops.push_back(Bcast{slot, slot, sizeof(int64_t) * (size_t)rows, r});
+        }
         if (nnz > 0) {
-            RCCL_TRY(R->Broadcast(me ? (const void *)Cl->col : nullptr, F.col + noff[r], (size_t)nnz, ncclInt32, r,
-                                  d->comm, s));
-            RCCL_TRY(R->Broadcast(me ? (const void *)Cl->val : nullptr, F.val + noff[r], (size_t)nnz, ncclFloat64, r,
-                                  d->comm, s));
+            ops.push_back(Bcast{me ? (const void *)(Cl->col + rp0) : nullptr, F.col + noff[r],
+                                sizeof(int32_t) * (size_t)nnz, r});
+            ops.push_back(Bcast{me ? (const void *)(Cl->val + rp0) : nullptr, F.val + noff[r],
+                                sizeof(double) * (size_t)nnz, r});
         }
     }
-    RCCL_TRY(R->GroupEnd());
-    HIPC(hipStreamSynchronize(s));
+    IAS_TRY(d->tr->bcast_group(ops, s));
+    IAS_TRY(hipc(hipStreamSynchronize(s)));
     *Cf = F;
+    guard.F = nullptr;
     return IAS_SUCCESS;
 }
 

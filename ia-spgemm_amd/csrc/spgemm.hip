@@ -6,6 +6,7 @@
 #include "spgemm_kernels.hpp"
 #include "onepass_kernels.hpp"
 #include "sym2_kernels.hpp"
+#include "sym3_kernels.hpp"
 #include "num2_kernels.hpp"
 #include <functional>
 #include "short_kernels.hpp"
@@ -201,6 +202,12 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
                 B.row(j[u], bs[u], bn[u]);
                 if (ax.aval) av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
             }
+        }
+        if (ax.wide_b) {
+            bool wide = false;
+#pragma unroll
+            for (int u = 0; u < AN_U; ++u) wide |= bs[u] + bn[u] > (1ll << 30);
+            if (wide) *ax.wide_b = 1;
         }
 #pragma unroll
         for (int u = 0; u < AN_U; ++u) {
@@ -1763,6 +1770,42 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
     }
 }
 
+// IAS_SYM3=0: the 257 .. 1024-product rows take sym2's teams instead of
+// sym3's one-wave rows (sym3_kernels.hpp).
+static bool sym3_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SYM3");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 1024;
+static int sym3_slot(int32_t upper) { return upper <= 512 ? 0 : (upper <= 768 ? 1 : 2); }
+#ifndef SYM3_WPB
+#define SYM3_WPB 4
+#endif
+#ifndef SYM3_DB_MAXK
+#define SYM3_DB_MAXK 8   // K up to which the next row's columns are gathered during a row (registers)
+#endif
+template <int K>
+static void sym3_launch(const Sym3Args &a, hipStream_t s) {
+    auto kern = k_sym3<K, SYM3_WPB, (K <= SYM3_DB_MAXK)>;
+    const int64_t want = ((int64_t)a.count + SYM3_WPB - 1) / SYM3_WPB;
+    const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM3_WPB, 0));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM3_WPB, 0, s>>>(a);
+}
+// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then sym2's 128-lane teams over
+// the rows it handed back (count read on the device)
+static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+    if (upper <= 512) sym3_launch<8>(a, s);
+    else if (upper <= 768) sym3_launch<12>(a, s);
+    else sym3_launch<16>(a, s);
+    retry.list = a.retry;
+    retry.count = a.count;   // grid bound; the device count decides
+    retry.count_dev = a.retry_count;
+    sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
+}
+
 template <int TEAM, int K, int SEG, int TPW, int PER>
 static void val_launch(const Launch &l, const Out &out) {
     auto kern = k_numeric_val<TEAM, K, SEG, TPW, PER>;
@@ -1988,7 +2031,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
         const int64_t per = (int64_t)AN_BLOCK * AN_U;
         const unsigned g = (unsigned)std::min<int64_t>((a_entries + per - 1) / per, 16384);
         k_an_entries<<<g, AN_BLOCK, 0, s>>>(A, B, a_entries,
-                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, axr});
+                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, axr, &dc->wide_b});
     }
     CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
@@ -2049,6 +2092,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PBOFF, sizeof(int64_t) * (size_t)(rows + 1)));
     IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
     if (part_bucket()) IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
+    if (sym3_on() && !c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -2107,7 +2151,17 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 continue;
             }
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
-                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl, DW_MAX};
+                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl, DW_MAX, nullptr};
+            if (sym3_on() && !c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
+                const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                                  &dc->s3_retry[sym3_slot(u)]};
+                Sym2Args r2 = a2;
+                r2.lay = sym2_layout(u, 4);   // the 128-lane team layout of this bound
+                sym3_bin(u, a3, r2, t);
+                CHECK_LAUNCH("k_sym3", t);
+                continue;
+            }
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);
         }
@@ -2243,8 +2297,13 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             CHECK_LAUNCH("k_numeric_dw", t);
         }
     }
-    // streaming rows: flat pass, then the duplicate fix-up (same stream, ordered)
+    // streaming rows: flat pass, then the duplicate fix-up (same stream, ordered).
+    // Fixed lanes (side stream 2 for the pass, 3 for its fix-ups and the short
+    // rows), whatever the bins before it: measured, the schedule is sensitive
+    // to which streams share a hardware queue (K3' numeric 5.33 vs 5.90 ms when
+    // an empty direct-write bin shifted the pass one stream down).
     if (n_entries > 0) {
+        if (!serial && !small && lane_no < 2) lane_no = 2;
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
         const FlatArgs fa{as<int32_t>(bufs[B_AXR]), as<int64_t>(bufs[B_AXP]), as<int64_t>(bufs[B_POFF]),
                           n_entries, as<int32_t>(bufs[B_TCOL]), bm, sa.dupn, sa.dup_off,

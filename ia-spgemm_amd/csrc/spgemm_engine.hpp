@@ -50,6 +50,8 @@ struct Counters {
     int32_t max_nnz;
     int32_t overflow;
     int32_t pad;
+    int32_t s3_retry[4];          // sym3: rows handed to sym2 per bin (retry lists)
+    int32_t wide_b;               // a selected B row ends beyond 2^30 entries: no sym3 (32-bit offsets)
     int32_t count[MAX_BINS];      // rows per bin (counting pass)
     int32_t cursor[MAX_BINS];     // scatter-pass cursors
 };
@@ -67,7 +69,9 @@ struct ias_plan {
         // partition buckets of the symbolic pass
         B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
         // work units of the row-unit numeric pass (num2)
-        B_N2CNT, B_N2OFF, B_N2UNIT, B_COUNT
+        B_N2CNT, B_N2OFF, B_N2UNIT,
+        // sym3's retry lists (rows whose possible-duplicate list overflowed)
+        B_S3RETRY, B_COUNT
     };
     struct Buf {
         void *p = nullptr;

@@ -126,6 +126,7 @@ struct AxOut {
     int32_t *blen;
     double *aval;
     int32_t *row;
+    int32_t *wide_b;   // nullable: set to 1 when a selected B row ends beyond 2^30 entries
 };
 
 // A row of a bin list: its first expanded-A entry and entry count.

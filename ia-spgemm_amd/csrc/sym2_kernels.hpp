@@ -99,6 +99,7 @@ struct Sym2Args {
     int32_t ablate;            // timing experiments only (IAS_S2_ABLATE): 2 no gathers
     int32_t bm_need;           // heavy rows above this nnz get dupn -3: the numeric pass's
                                // partitioned path needs a bitmap they do not have
+    const int32_t *count_dev;  // non-null: the row count is read here (sym3's retry list)
 };
 
 // What a team prefetches of a row before it works on it.
@@ -167,7 +168,9 @@ __device__ __forceinline__ uint32_t fib(int32_t c) { return (uint32_t)c * 0x9E37
 // WPE: minimum waves per SIMD the register allocation must allow (one-wave
 // teams with K >= 16 would otherwise take 160-256 VGPRs, 2 waves per SIMD).
 template <int TEAM, int K, int TPW, int WPE>
-__global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sym2(Sym2Args a) {
+__global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sym2(Sym2Args a0) {
+    Sym2Args a = a0;
+    if (a0.count_dev) a.count = *a0.count_dev;
     static_assert(TEAM >= WAVE && (TEAM <= WAVE || TPW == 1), "teams are whole waves; multi-wave teams own the WG");
     static_assert(TEAM == WAVE ? K <= 32 : K <= 16, "finish() covers the bitmap words in one pass");
     using TM = Team<TEAM>;

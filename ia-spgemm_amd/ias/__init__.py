@@ -105,7 +105,7 @@ EXPORTS = [
     "ias_csr_mul_csr_nnz", "ias_csr_mul_csr_compute", "ias_csr_mul_csr_into",
     "ias_flops", "ias_sum_csr", "ias_sum_coo", "ias_sum_ell", "ias_sum_dia",
     "ias_csr_row_view", "ias_partition_rows", "ias_row_ptr_shift",
-    "ias_csr_mul_csr_multi", "ias_dist_unique_id", "ias_dist_create", "ias_dist_destroy",
+    "ias_csr_mul_csr_multi", "ias_dist_unique_id", "ias_dist_create", "ias_dist_create_loopback", "ias_dist_destroy",
     "ias_dist_allgatherv_csr", "ias_dist_csr_mul_csr",
     "ias_gen_rmat", "ias_gen_band", "ias_gen_ell",
     "ias_mkl_available", "ias_mkl_sp2m",
@@ -169,6 +169,7 @@ def _load():
         "ias_csr_mul_csr_multi": (C.c_int, [P(Csr), P(Csr), P(Csr), C.c_int32, i32p, P(Opts), P(Report)]),
         "ias_dist_unique_id": (C.c_int, [C.c_char_p, C.c_int32]),
         "ias_dist_create": (C.c_int, [P(C.c_void_p), C.c_char_p, C.c_int32, C.c_int32, C.c_int32]),
+        "ias_dist_create_loopback": (C.c_int, [P(C.c_void_p), C.c_char_p, C.c_int32, C.c_int32, C.c_int32]),
         "ias_dist_destroy": (C.c_int, [C.c_void_p]),
         "ias_dist_allgatherv_csr": (C.c_int, [C.c_void_p, P(Csr), P(Csr), C.c_void_p]),
         "ias_dist_csr_mul_csr": (C.c_int, [C.c_void_p, P(Csr), P(Csr), P(Csr), C.c_int32, C.c_int32,

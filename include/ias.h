@@ -341,6 +341,14 @@ ias_status ias_csr_mul_csr_multi(const ias_csr *A, const ias_csr *B, ias_csr *C,
 typedef struct ias_dist ias_dist;
 ias_status ias_dist_unique_id(char *id, int32_t id_len);
 ias_status ias_dist_create(ias_dist **dist, const char *id, int32_t nranks, int32_t rank, int32_t device);
+/* The same rank handle over the in-process loopback transport (SURVEY.md
+ * §4.4): nranks ranks of ONE process, each driven by its own host thread, meet
+ * under the name `group`; the collectives are host barriers + hipMemcpyAsync
+ * of the peers' buffers.  Ranks may share a device (RCCL allows one rank per
+ * device), so the sharded path and the allgatherv fix-up run at P > 1 on one
+ * GPU.  Every other ias_dist_* entry point takes either kind of handle. */
+ias_status ias_dist_create_loopback(ias_dist **dist, const char *group, int32_t nranks, int32_t rank,
+                                    int32_t device);
 ias_status ias_dist_destroy(ias_dist *dist);
 /* Concatenate the row-sharded C on every rank: C_local (device, this rank's
  * rows, row pointer from 0) -> C_full (library-allocated on the rank's

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Call one GPU parity test function N times in one process (flakiness
-check; prints pass/fail per repetition).  usage: repeat_test.py N module func [args...]"""
+check; prints pass/fail per repetition).  usage: rerun_gpu_case.py N module func [args...]"""
 import importlib
 import os
 import sys
