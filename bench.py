@@ -74,6 +74,10 @@ def parse(argv=None):
                         "operands (banded configs, N=1)")
     p.add_argument("--no-gather", action="store_true", help="N>1: skip the allgatherv measurement")
     p.add_argument("--gather-reps", type=int, default=1, help="N>1: repetitions of the allgatherv measurement")
+    p.add_argument("--no-anchor", action="store_true",
+                   help="N>1: skip timing the whole matrix on rank 0's GPU alone after the distributed loop")
+    p.add_argument("--no-one-shot", action="store_true",
+                   help="N=1: skip the library-allocated one-shot calls (ias_csr_mul_csr, device C)")
     return p.parse_args(argv)
 
 
@@ -379,8 +383,24 @@ def main(argv=None):
     shards = as_ranks if as_ranks is not None else [rank]
     for shard in shards:
         out, step, cbufs = run_shard(shard)
+        out["value_per_gpu"] = round(out["value"] / max(1, out["n_gpus"]), 3)
         if dist_on and not args.no_gather:
             out["allgatherv"] = measure_allgatherv(step, *cbufs, args.gather_reps)
+        if dist_on and not args.no_anchor:
+            # the same matrix on one GPU (rank 0's, the others idle at a
+            # barrier), after the distributed loop: the scaling anchor
+            del cbufs, step
+            step = cbufs = None
+            torch.cuda.empty_cache()
+            anchor = same_matrix_1gpu(plan, dcsr(0, rows, rp, nnz_a), Bm, rows, cols, local, dev, rank,
+                                      out["ms_per_step"], flops_total)
+            if rank == 0:
+                out["same_matrix_1gpu"] = anchor
+        if rank == 0 and world == 1 and as_ranks is None and not args.no_one_shot:
+            del cbufs, step
+            step = cbufs = None
+            torch.cuda.empty_cache()
+            out["one_shot"] = one_shot(dcsr(0, rows, rp, nnz_a), local, out["ms_per_step"])
         if rank == 0 and world == 1 and as_ranks is None and not args.no_cpu_baseline and \
                 kind in ("rmat", "band", "ell"):
             out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
@@ -418,6 +438,79 @@ def main(argv=None):
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def same_matrix_1gpu(plan, Afull, Bm, rows, cols, local, dev, rank, ms_dist, flops_total, steps=2):
+    """Rank 0 computes the WHOLE C = A*A alone on its GPU (2 timed steps after
+    a warm-up, the same two-phase calls as a bench step) while the other ranks
+    wait at a barrier: the same-problem anchor of the N-GPU line
+    (speedup_vs_1gpu_same_matrix = t_1gpu / t_step).  Skipped when the whole
+    C does not fit next to what rank 0 holds."""
+    import torch
+    import torch.distributed as dist
+    import ias
+    res = None
+    dist.barrier()
+    if rank == 0:
+        nnz_c = C.c_int64(0)
+        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Afull), C.byref(Bm), C.byref(nnz_c), None, None), "nnz")
+        need = 12 * int(nnz_c.value) + 8 * (rows + 1)
+        free = torch.cuda.mem_get_info(dev)[0]
+        if need > 0.85 * free:
+            res = {"what": "skipped: the whole C does not fit on one GPU next to the workspace",
+                   "c_bytes": need, "free_bytes": free}
+        else:
+            c_rp = torch.empty(rows + 1, dtype=torch.int64, device=dev)
+            c_ci = torch.empty(max(int(nnz_c.value), 1), dtype=torch.int32, device=dev)
+            c_va = torch.empty(max(int(nnz_c.value), 1), dtype=torch.float64, device=dev)
+            Cm = ias.Csr(rows, cols, int(nnz_c.value), C.cast(C.c_void_p(c_rp.data_ptr()), ias.i64p),
+                         C.cast(C.c_void_p(c_ci.data_ptr()), ias.i32p),
+                         C.cast(C.c_void_p(c_va.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
+
+            def step():
+                n = C.c_int64(0)
+                ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Afull), C.byref(Bm), C.byref(n), None, None),
+                          "nnz")
+                ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Afull), C.byref(Bm), C.byref(Cm), 0, None),
+                          "compute")
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            torch.cuda.synchronize()
+            ms1 = 1e3 * (time.perf_counter() - t0) / steps
+            del c_rp, c_ci, c_va
+            torch.cuda.empty_cache()
+            res = {"what": "the whole matrix C = A*A on rank 0's GPU alone (same two-phase calls), after the "
+                           "distributed loop", "ms_per_step": round(ms1, 3),
+                   "gflops": round(2.0 * flops_total / (ms1 * 1e6), 3), "steps": steps,
+                   "speedup_vs_1gpu_same_matrix": round(ms1 / ms_dist, 3)}
+    dist.barrier()
+    return res
+
+
+def one_shot(Am, local, ms_step):
+    """Two ias_csr_mul_csr calls with device-resident A = B and a device C the
+    library allocates (no plan, no stream passed: the per-device default plan),
+    as the reference's cuSPARSE timed region includes C's allocation
+    (GPU/detail/cusparse/common_cusparse.h:74-93): wall and device ms of the
+    first call (workspace allocation included) and of the second."""
+    import ias
+    res = {}
+    for tag in ("first", "second"):
+        c, rep = ias.Csr(), ias.Report()
+        o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=local)
+        t = time.perf_counter()
+        ias.check(ias.lib.ias_csr_mul_csr(C.byref(Am), C.byref(Am), C.byref(c), C.byref(o), C.byref(rep)),
+                  "one-shot")
+        res[f"ms_wall_{tag}"] = round(1e3 * (time.perf_counter() - t), 3)
+        res[f"ms_device_{tag}"] = round(rep.ms_total, 3)
+        ias.lib.ias_csr_free(C.byref(c))
+    res["what"] = ("ias_csr_mul_csr, device A = B, library-allocated device C (C's allocation inside the call, "
+                   "as cuSPARSE's timed region), default plan; wall includes the call's host work")
+    res["first_vs_warm_step"] = round(res["ms_wall_first"] / ms_step, 3)
+    return res
 
 
 def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):

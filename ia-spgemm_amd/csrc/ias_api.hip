@@ -426,17 +426,66 @@ extern "C" ias_status ias_dia_copy(const ias_dia *src, ias_dia *dst, int32_t mem
 // =================================================================== SpGEMM
 namespace {
 
-// A temporary plan when the caller did not pass one.
+// When the caller passes no plan (and no stream), a per-device default plan
+// kept for the life of the process serves the call — as a cuSPARSE handle
+// would — so repeated one-shot calls do not re-create streams, events and the
+// workspace (the first K3' call spent ~120 ms of its 133 ms there).  A call
+// that finds the default plan busy (another host thread) or brings its own
+// stream gets a temporary plan.  IAS_DEFAULT_PLAN=0 always uses temporaries.
+struct DefaultPlans {
+    std::mutex mu;
+    std::map<int, ias_plan *> plan;
+    std::map<int, bool> busy;
+};
+DefaultPlans &default_plans() {
+    static DefaultPlans *d = new DefaultPlans;   // never destroyed (plans may be in use at exit)
+    return *d;
+}
+bool default_plan_on() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_DEFAULT_PLAN");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 struct PlanGuard {
     ias_plan *p = nullptr;
-    bool owned = false;
+    bool owned = false, pooled = false;
+    int dev = 0;
     ~PlanGuard() {
         if (owned) ias_plan_destroy(p);
+        if (pooled) {
+            DefaultPlans &d = default_plans();
+            std::lock_guard<std::mutex> g(d.mu);
+            d.busy[dev] = false;
+        }
     }
     ias_status acquire(const ias_opts &o, int device) {
         if (o.plan) {
             p = o.plan;
             return IAS_SUCCESS;
+        }
+        if (!o.stream && default_plan_on()) {
+            DefaultPlans &d = default_plans();
+            std::unique_lock<std::mutex> g(d.mu);
+            if (!d.busy[device]) {
+                ias_plan *&dp = d.plan[device];
+                if (!dp) {
+                    g.unlock();
+                    ias_plan *np = nullptr;
+                    IAS_TRY(ias_plan_create(&np, device, nullptr));
+                    g.lock();
+                    if (!dp) dp = np;
+                    else ias_plan_destroy(np);
+                }
+                if (!d.busy[device]) {
+                    d.busy[device] = true;
+                    pooled = true;
+                    dev = device;
+                    p = dp;
+                    return IAS_SUCCESS;
+                }
+            }
         }
         owned = true;
         return ias_plan_create(&p, device, o.stream);

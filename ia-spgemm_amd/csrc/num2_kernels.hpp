@@ -86,11 +86,19 @@ __global__ void k_num2_fill(int64_t rows, const int32_t *cnt, const int64_t *uof
     for (int32_t j = 0; j < c; ++j) units[o + j] = Num2Unit{r, j * N2_ENT};
 }
 
+// Timing-only ablations (never shipped; tools/build_variants.sh): 1 = no C
+// stores, 2 = no B gathers (column = product, value 1), 4 = plain (not
+// non-temporal) C stores.
+#ifndef N2_ABLATE
+#define N2_ABLATE 0
+#endif
 // 16-byte non-temporal store (C is not read back by this pass)
 typedef uint32_t n2_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st16(void *p, uint4 v) {
     const n2_u32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, (n2_u32x4 *)p);
+    if (N2_ABLATE & 1) return;
+    if (N2_ABLATE & 4) *(n2_u32x4 *)p = x;
+    else __builtin_nontemporal_store(x, (n2_u32x4 *)p);
 }
 
 // N2_K windows per step: their gathers are in flight together, and the next
@@ -188,8 +196,13 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
             const int ecur = __popcll(__ballot(bl > 0 && rel < pw));
             S.e[k] = max(ecur + __popcll(wmask[w][k] & upto) - 1, 0);
             const int64_t kb = (p >= pa && p < pb) ? ent[w][S.e[k]].bs + p : 0;
-            S.c[k] = a.bcol[kb];
-            S.bv[k] = a.bval[kb];
+            if (N2_ABLATE & 2) {
+                S.c[k] = p;
+                S.bv[k] = 1.0;
+            } else {
+                S.c[k] = a.bcol[kb];
+                S.bv[k] = a.bval[kb];
+            }
             const int64_t wi = min(bmo + (pw >> 5) + (lane >> 5), lastw);
             S.word[k] = a.bm.bits[wi];
             S.pre[k] = a.bm.pref[wi];
@@ -252,8 +265,10 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
         else if (lane < 6) xc = max(e4, a4) + (lane - 3) < xhi ? max(e4, a4) + (lane - 3) : -1;
         else if (lane == 6) xv = xlo < min(a2, xhi) ? xlo : -1;
         else if (lane == 7) xv = max(e2, a2) < xhi ? max(e2, a2) : -1;
-        if (xc >= 0) __builtin_nontemporal_store(scol[w][idx(xc)], &out.col[xc]);
-        if (xv >= 0) __builtin_nontemporal_store(sval[w][idx(xv)], &out.val[xv]);
+        if (!(N2_ABLATE & 1)) {
+            if (xc >= 0) __builtin_nontemporal_store(scol[w][idx(xc)], &out.col[xc]);
+            if (xv >= 0) __builtin_nontemporal_store(sval[w][idx(xv)], &out.val[xv]);
+        }
         r0 += nft;
         wave_sync();
     };

@@ -1779,8 +1779,10 @@ static bool sym3_on() {
     }();
     return on;
 }
-constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 1024;
-static int sym3_slot(int32_t upper) { return upper <= 512 ? 0 : (upper <= 768 ? 1 : 2); }
+#ifndef SYM3_MAX_DEF
+#define SYM3_MAX_DEF 2048
+#endif
+constexpr int32_t SYM3_MIN = 257, SYM3_MAX = SYM3_MAX_DEF;
 #ifndef SYM3_WPB
 #define SYM3_WPB 4
 #endif
@@ -1799,11 +1801,14 @@ static void sym3_launch(const Sym3Args &a, hipStream_t s) {
 static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
     if (upper <= 512) sym3_launch<8>(a, s);
     else if (upper <= 768) sym3_launch<12>(a, s);
-    else sym3_launch<16>(a, s);
+    else if (upper <= 1024) sym3_launch<16>(a, s);
+    else if (upper <= 1536) sym3_launch<24>(a, s);
+    else sym3_launch<32>(a, s);
     retry.list = a.retry;
     retry.count = a.count;   // grid bound; the device count decides
     retry.count_dev = a.retry_count;
-    sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
+    if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
+    else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
 }
 
 template <int TEAM, int K, int SEG, int TPW, int PER>
@@ -2155,9 +2160,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             if (sym3_on() && !c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
                 const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
-                                  &dc->s3_retry[sym3_slot(u)]};
+                                  &dc->s3_retry[b & 7]};   // a counter per bin (bins run concurrently)
                 Sym2Args r2 = a2;
-                r2.lay = sym2_layout(u, 4);   // the 128-lane team layout of this bound
+                r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
                 sym3_bin(u, a3, r2, t);
                 CHECK_LAUNCH("k_sym3", t);
                 continue;

@@ -69,19 +69,22 @@ struct Sym3Lds {
     static constexpr int F1B = 16 * U;     // f1 bits
     static constexpr int F1W = F1B / 32;
     static constexpr int F2B = 2 * U;      // f2 bits
-    static constexpr int F2W = F2B / 32;   // >= 2K: also the bitmap words' OR scratch
+    static constexpr int F2W = F2B / 32;   // >= 2K: its first words also hold the bitmap words (exact phase)
     static constexpr int NE = WAVE;        // A entries per row at most (one per lane)
     static constexpr int LC = U / 8;       // possible-duplicate list capacity
-    static constexpr int ES = 2 * LC;      // exact-table slots
+    static constexpr int ES = LC;          // exact-table slots (the list is at most 3/4 full)
     static constexpr int LT = (LC + WAVE - 1) / WAVE;   // list entries per lane
-    static_assert(8 * LC <= 4 * F1W, "the list overlays f1");
-    static_assert(F2W >= 2 * K && F2W <= WAVE, "f2 holds the bitmap words during the exact phase");
+    // after classification f1 is free: the list (8 B per entry) and the exact
+    // table (column + first product, 8 B per slot) live there
+    static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
+    static_assert(F2W >= 2 * K && 2 * K <= WAVE, "bitmap words: one per lane");
     __attribute__((aligned(16))) uint32_t f1[F1W];
     __attribute__((aligned(16))) uint32_t f2[F2W];
-    __attribute__((aligned(16))) int32_t keys[ES];
-    __attribute__((aligned(16))) uint32_t own[ES];
-    int32_t ebase[NE];              // B-row start - first product (B has < 2^31 - 2^16 entries)
+    int32_t ebase[NE];              // B-row start - first product (B has < 2^30 entries)
     unsigned long long mask[K];
+    __device__ int2 *list() { return (int2 *)f1; }
+    __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
+    __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
 };
 
 // A row as a wave holds it before resolving it.
@@ -186,11 +189,11 @@ __device__ __forceinline__ void s3_gather(const Sym3Args &a, Sym3Lds<K> &L, cons
     }
 }
 
-#ifndef SYM3_WPE
-#define SYM3_WPE 5   // waves per SIMD the register allocation must allow
-#endif
+// waves per SIMD the register allocation must allow (K columns per lane)
+template <int K>
+constexpr int sym3_wpe() { return K <= 8 ? 5 : (K <= 16 ? 4 : 3); }
 template <int K, int WPB, bool DB>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_WPE))) void k_sym3(Sym3Args a) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_wpe<K>()))) void k_sym3(Sym3Args a) {
     using LDS = Sym3Lds<K>;
     constexpr int CH = K < 8 ? K : (K % 8 == 0 ? 8 : (K % 6 == 0 ? 6 : 4));   // filter chunk: products per lane whose LDS atomics fly together
     static_assert(K % CH == 0, "K in whole chunks");
@@ -203,31 +206,26 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
     int64_t idx = (int64_t)blockIdx.x * WPB + w;
     if (idx >= a.count) return;
     for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
-    if (lane < LDS::F2W) L.f2[lane] = 0u;
+    for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
     s3_sync();
 
-    // Pipeline (row i = cur): list entries two rows ahead, details (+ DB:
-    // the columns) one row ahead; one full wait per row at the top, so no
-    // wait inside an iteration stalls on loads issued for later rows.
     // Pipeline, row i = cur.  DB: list entries two rows ahead, details and
-    // columns one row ahead (row i+1's gathers fly while row i is resolved).
-    // Otherwise: the list entry one row ahead, row i+1's details loaded at
-    // the top of row i and its columns gathered at the end.  One full wait
-    // per row at the top, so no wait inside an iteration stalls on loads
-    // issued for later rows.
+    // columns one row ahead (row i+1's gathers fly while row i is resolved;
+    // twice the column registers).  Otherwise row i+1's columns are gathered
+    // into the same registers as soon as row i's classification no longer
+    // needs them, so they fly during row i's exact phase and finish, and row
+    // i+2's details with them.
     Sym3Row cur = s3_load(a, s3_ref(a, idx));
     int32_t c[K];
     s3_gather<K>(a, L, cur, c);
-    Sym3Row nxt;
-    RowRef nref;
-    if constexpr (DB) {
-        nxt = s3_load(a, s3_ref(a, idx + stride));
-        nref = s3_ref(a, idx + 2 * stride);
-    } else {
-        nref = s3_ref(a, idx + stride);
-    }
+    Sym3Row nxt = s3_load(a, s3_ref(a, idx + stride));
+    RowRef nref = s3_ref(a, idx + 2 * stride);
+    Timer tm;   // timing builds only (phases: 0 top wait, 1 next row's gather / details issue (DB),
+                // 2 filter, 3 classify + list, 4 exact, 5 finish, 6 filter clear, 7 next row's gather)
+    tm.start();
     while (true) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): row i's columns, what is prefetched
+        if constexpr (DB) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): row i's columns, row i+1's details
+        tm.mark(0);
         const int32_t row = __builtin_amdgcn_readfirstlane(cur.ref.row);
         if (row < 0) break;
         const int32_t P = __builtin_amdgcn_readfirstlane(cur.P);
@@ -241,10 +239,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
             s3_gather<K>(a, L, nxt, cn);   // nxt.row < 0: dummy loads of B.col[0]
             nn = s3_load(a, nref);
             nref = s3_ref(a, idx + 3 * stride);
-        } else {
-            nxt = s3_load(a, nref);
-            nref = s3_ref(a, idx + 2 * stride);
         }
+        tm.mark(1);
 
         // ---- filter: f1 with return, candidates mark f2 (CH items at a time)
         uint32_t candm = 0u;
@@ -270,6 +266,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
             }
         }
         s3_sync();
+        tm.mark(2);
         // ---- classify: certain first touches -> bitmap words in the lanes,
         // possible duplicates -> list (product order) over f1
         uint32_t wd = 0u;   // lane j: bitmap word j
@@ -295,7 +292,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
             }
         }
         s3_sync();   // every f1 / f2 read done before the list overwrites f1
-        int2 *list = (int2 *)L.f1;
+        int2 *list = L.list();
+        int32_t *keys = L.keys();
+        uint32_t *own = L.own();
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const bool poss = (possm >> k) & 1u;
@@ -307,12 +306,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
             nl += __popcll(pb);
         }
         const int32_t row_nw = (P + 31) >> 5;
-        const bool retry = nl > LDS::LC || P > LDS::U || nent > WAVE;
+        tm.mark(3);
+        if constexpr (!DB) {
+            // row i's columns are dead: row i+1's gathers fly from here on
+            s3_gather<K>(a, L, nxt, c);
+            nn = s3_load(a, nref);
+            nref = s3_ref(a, idx + 3 * stride);
+            tm.mark(7);
+        }
+        const bool retry = 4 * nl > 3 * LDS::LC || P > LDS::U || nent > WAVE;
         if (nl > 0 && !retry) {
             // ---- exact: claim the column (CAS, linear probing); its smallest
             // product is the first touch
-            for (int i = lane; i < LDS::ES; i += WAVE) L.keys[i] = EMPTY_KEY;
-            if (lane < LDS::F2W) L.f2[lane] = lane < 2 * K ? wd : 0u;   // bitmap words -> LDS (f2 is done)
+            for (int i = lane; i < LDS::ES; i += WAVE) keys[i] = EMPTY_KEY;
+            for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = i < 2 * K ? wd : 0u;   // bitmap words -> LDS (f2 is done)
             s3_sync();
             int2 e[LDS::LT];
             uint32_t slot[LDS::LT];
@@ -327,7 +334,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
                     uint32_t s = s3_h3(e[t].x, LDS::ES);
                     bool won = false;
                     for (int probe = 0; probe < LDS::ES; ++probe) {
-                        const int32_t g = atomicCAS(&L.keys[s], EMPTY_KEY, e[t].x);
+                        const int32_t g = atomicCAS(&keys[s], EMPTY_KEY, e[t].x);
                         if (g == EMPTY_KEY) {
                             won = true;
                             break;
@@ -336,27 +343,28 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
                         s = s + 1u == (uint32_t)LDS::ES ? 0u : s + 1u;
                     }
                     slot[t] = s;
-                    if (won) L.own[s] = (uint32_t)e[t].y;
+                    if (won) own[s] = (uint32_t)e[t].y;
                     wonm |= (won ? 1u : 0u) << t;
                 }
             }
             s3_sync();
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t)
-                if (t * WAVE + lane < nl && !((wonm >> t) & 1u)) atomicMin(&L.own[slot[t]], (uint32_t)e[t].y);
+                if (t * WAVE + lane < nl && !((wonm >> t) & 1u)) atomicMin(&own[slot[t]], (uint32_t)e[t].y);
             s3_sync();
             uint32_t f[LDS::LT];
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t) {
                 f[t] = 0;
                 if (t * WAVE + lane < nl) {
-                    f[t] = L.own[slot[t]];
+                    f[t] = own[slot[t]];
                     const uint32_t p = (uint32_t)e[t].y;
                     if (f[t] == p) atomicOr(&L.f2[p >> 5], 1u << (p & 31));
                 }
             }
             s3_sync();
             wd = lane < 2 * K ? L.f2[lane] : 0u;
+            tm.mark(4);
             // ---- finish with duplicates
             const uint32_t cnt = lane < row_nw ? (uint32_t)__popc(wd) : 0u;
             const int incl = wave_incl_sum((int)cnt);
@@ -403,21 +411,22 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM3_W
             a.retry[j] = cref;
         }
         // ---- the filters empty for the next row
+        tm.mark(5);
         s3_sync();
         for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
-        if (lane < LDS::F2W) L.f2[lane] = 0u;
+        for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
         s3_sync();
+        tm.mark(6);
         if constexpr (DB) {
 #pragma unroll
             for (int k = 0; k < K; ++k) c[k] = cn[DB ? k : 0];
-            cur = nxt;
-            nxt = nn;
-        } else {
-            s3_gather<K>(a, L, nxt, c);
-            cur = nxt;
         }
+        cur = nxt;
+        nxt = nn;
+        tm.done();
         idx += stride;
     }
+    tm.flush(24 + (K >= 16 ? 2 : (K >= 12 ? 1 : 0)), lane == 0);
 }
 
 }  // namespace dev

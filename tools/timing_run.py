@@ -47,7 +47,9 @@ def main():
             continue
         kind = "symbolic" if slot < 16 else "numeric"
         team = 1 << (slot % 16)
-        if slot >= 30:
+        if 24 <= slot <= 26:
+            kind, team = "sym3 K=%d" % (8, 12, 16)[slot - 24], 64
+        elif slot >= 30:
             kind, team = ("onepass" if slot == 31 else "op-big"), 512
         elif slot == 29:
             kind, team = "sym-part", 1024
