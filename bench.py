@@ -3,13 +3,14 @@
 
 Contract:
   python bench.py --gpus N --steps K --warmup W
-One step = one full C = A*A of this rank's row block through the C-ABI
-two-phase entry points (ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, as
-cuSPARSE's csrgemmNnz + csrgemm: row analysis, binning, symbolic, scan, host
-read of nnz, numeric + write C), inputs resident in HBM, C written into
-preallocated device arrays.  `--engine onepass` times the single-pass chunk
-engine instead (ias_csr_mul_csr_into with IAS_ONEPASS=1; C's capacity =
-flops(A*A) >= nnz(C), reported by a capacity-0 call before timing).
+One step = one full C = A*A of this rank's row block through the C-ABI,
+inputs resident in HBM, C written into preallocated device arrays.  Default
+`--engine pipe`: one ias_csr_mul_csr_into call per step (C's capacity =
+flops(A*A) >= nnz(C)), the library's row-block pipeline — A's rows in 4
+blocks, each block's symbolic pass beside the previous block's numeric pass.
+`--engine twophase`: ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, as
+cuSPARSE's csrgemmNnz + csrgemm (row analysis, binning, symbolic, scan, host
+read of nnz, numeric + write C).
 
 Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15.
 N=1: the north-star headline matrix K3' (2^20 rows, edge factor 20, seed 2;
@@ -62,7 +63,10 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
-    p.add_argument("--engine", default="twophase", choices=["onepass", "twophase"])
+    p.add_argument("--engine", default="pipe", choices=["pipe", "twophase"],
+                   help="pipe: one ias_csr_mul_csr_into call per step (row blocks, each block's symbolic "
+                        "pass overlapping the previous block's numeric pass); twophase: ias_csr_mul_csr_nnz + "
+                        "ias_csr_mul_csr_compute")
     p.add_argument("--no-host-e2e", action="store_true",
                    help="skip the one PCIe-inclusive call with host operands (N=1 only)")
     p.add_argument("--as-rank", default=None,
@@ -188,8 +192,6 @@ def main(argv=None):
     plan = C.c_void_p()
     ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
     order = ias.ORDER_SORTED if args.order == "sorted" else ias.ORDER_REFERENCE
-    if args.engine == "onepass":
-        os.environ["IAS_ONEPASS"] = "1"
 
     def run_shard(shard):
         """Warm-up + the timed loop over this process's shard `shard` of A;
@@ -203,17 +205,12 @@ def main(argv=None):
                       "nnz")
             cap = int(nnz_c.value)
         else:
-            # capacity = flops of this shard (an upper bound of nnz(C) known from A and B alone):
-            # a capacity-0 call reports it without writing C
-            probe = ias.Report()
-            c_rp0 = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
-            C0 = ias.Csr(r1 - r0, cols, 0, C.cast(C.c_void_p(c_rp0.data_ptr()), ias.i64p), None, None,
-                         ias.MEMORY_DEVICE, local)
-            st = ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(C0), 0, C.byref(probe))
-            if st not in (0, 11):
-                ias.check(st, "into (capacity probe)")
+            # capacity = flops of this shard, an upper bound of nnz(C) known from
+            # A and B alone (here read off a symbolic pass's report)
+            nnz_c, probe = C.c_int64(0), ias.Report()
+            ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Bm), C.byref(nnz_c), None,
+                                                  C.byref(probe)), "nnz (capacity probe)")
             cap = int(probe.flops)
-            del c_rp0
         c_rp = torch.empty(r1 - r0 + 1, dtype=torch.int64, device=dev)
         c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
         c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
@@ -223,7 +220,7 @@ def main(argv=None):
         rep = ias.Report()
         rep_s = ias.Report()
 
-        def step_onepass():
+        def step_pipe():
             Cm.nnz = cap
             ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
                                                    C.byref(rep)), "into")
@@ -239,7 +236,7 @@ def main(argv=None):
             rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
             return rep
 
-        step = step_onepass if args.engine == "onepass" else step_twophase
+        step = step_pipe if args.engine == "pipe" else step_twophase
 
         for _ in range(args.warmup):
             step()
@@ -257,8 +254,17 @@ def main(argv=None):
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        local_nnz = int(Cm.nnz) if args.engine == "pipe" else cap
+        if args.engine == "pipe":
+            # phases and the dominant kernel's event timing come from two-phase
+            # steps after the timed loop (one call per step leaves no phase
+            # boundary: symbolic and numeric blocks overlap)
+            reps = []
+            for _ in range(2):
+                r = step_twophase()
+                reps.append((r.ms_total, r.ms_analysis, r.ms_symbolic, r.ms_numeric, r.ms_stream))
+            Cm.nnz = local_nnz
         t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        local_nnz = int(Cm.nnz) if args.engine == "onepass" else cap
         nnz_tot = torch.tensor([float(local_nnz)], dtype=torch.float64, device=dev)
         num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
         if dist_on:
@@ -271,7 +277,7 @@ def main(argv=None):
         nnz_c_total = int(nnz_tot.item())
 
         # Roofline (HBM-bound).  Dominant launch: the streaming
-        # numeric pass (k_num2; k_onepass for --engine onepass), event-timed on
+        # numeric pass (k_num2), event-timed on
         # its own stream inside the library.  Its algorithmic bytes per launch
         # follow §8(d3)'s B_alg: the C entries it writes (12 B each) plus one
         # read of A and of B (bytes(X) = 8·(rows+1) + 12·nnz(X)); the B-row
@@ -285,15 +291,14 @@ def main(argv=None):
         ms_flat = statistics.mean(x[4] for x in reps)
         flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
         gather_bytes = 12 * int(rep.stream_products)
-        kname = "k_onepass" if args.engine == "onepass" else \
-            ("k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2")
+        kname = "k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2"
         units = {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)}
         # the pass is 1 to 3 launches (rows by duplicate class; each class's
         # fix-ups overlap the rest): ms_stream sums the launches' own durations
         # (events around each launch), so per launch = the pass's bytes and time
         # / launches, which is what rocprofv3's average launch duration shows
         launches = max(1, int(getattr(rep, "stream_launches", 1) or 1))
-        if args.engine == "twophase" and int(rep.stream_nnz) < local_nnz // 2:
+        if int(rep.stream_nnz) < local_nnz // 2:
             # most of C comes from the short-row / table kernels (K1, K2): the
             # dominant unit is then the whole numeric phase (event-timed), its
             # bytes the C entries it writes plus one read of A and B
@@ -372,7 +377,7 @@ def main(argv=None):
         if as_ranks is not None:
             out["as_rank"] = {"rank": shard, "of": world_req, "rows": [r0, r1],
                               "note": "one rank's shard only: value / nnz_per_s are per-rank figures"}
-            shard_flops = int(rep_s.flops) if args.engine == "twophase" else int(rep.flops)
+            shard_flops = int(rep_s.flops) if args.engine in ("twophase", "pipe") else int(rep.flops)
             out["as_rank"]["flops"] = shard_flops
             out["as_rank"]["nnz_c"] = local_nnz
             out["value"] = round(2.0 * shard_flops / (ms_step * 1e6), 3)

@@ -547,21 +547,6 @@ int pick_device(const ias_opts &o, int a_mem, int a_dev) {
     return 0;
 }
 
-// IAS_ONEPASS=1 selects the single-pass chunk engine (onepass_kernels.hpp)
-// for CSR products; the default is the two-phase engine, faster on skewed
-// (power-law) inputs where most products sit in rows too long for a chunk.
-bool onepass_enabled() {
-    const char *e = getenv("IAS_ONEPASS");
-    return e && *e == '1';
-}
-
-// A C allocated at its upper bound (flops entries of 12 B) must leave room.
-bool onepass_fits(int64_t flops) {
-    size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
-    return 12.0 * (double)flops + 8.0 <= 0.5 * (double)fr;
-}
-
 // host wall clock (ms) for the synchronous PCIe staging of host operands
 double host_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -606,29 +591,14 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     dev::Rows ra{dA->row_ptr, nullptr, 0, dA->col, dA->val};
     dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
     ias_csr D{};
-    ias_status stn = IAS_SUCCESS;
-    bool done = false;
     plan->last_a = plan->last_b = nullptr;
-    if (onepass_enabled()) {
-        // single pass into C allocated at its upper bound flops(A*B) >= nnz(C)
-        IAS_TRY(plan->onepass_prepare(ra, rb, A->rows, B->cols, dA->nnz, rep));
-        if (onepass_fits(plan->flops)) {
-            IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, plan->flops, IAS_MEMORY_DEVICE, plan->device));
-            int64_t nnz = 0;
-            stn = plan->onepass_run(ra, rb, D.row_ptr, D.col, D.val, plan->flops, 0, 0, &nnz, rep);
-            D.nnz = nnz;
-            done = true;
-        }
-    }
-    if (!done) {
-        IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
-        const int64_t nnz = plan->nnz_total;
-        IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
-        HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
-                            hipMemcpyDeviceToDevice, s));
-        dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0, nullptr};
-        stn = plan->numeric(ra, rb, out, rep);
-    }
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
+    const int64_t nnz = plan->nnz_total;
+    IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
+    HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                        hipMemcpyDeviceToDevice, s));
+    dev::Out out{D.row_ptr, 0, D.col, D.val, nullptr, 0, 0, nullptr};
+    ias_status stn = plan->numeric(ra, rb, out, rep);
     if (stn == IAS_SUCCESS && o.order == IAS_ORDER_SORTED)
         stn = ias_sort_rows_device(plan, D.row_ptr, A->rows, D.col, D.val, plan->max_nnz);
     if (stn != IAS_SUCCESS) {
@@ -858,6 +828,20 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
     return IAS_SUCCESS;
 }
 
+// Row blocks of the one-call pipeline (IAS_PIPE_BLOCKS, default 4; 1 = off):
+// only for products big enough that a block keeps the GPU busy (A with at
+// least IAS_PIPE_MIN entries, default 4M — the knob lets the parity tests run
+// small inputs through it), and never in the plan's serial (profiling) mode.
+// Read per call (one getenv each: the tests switch them between cases).
+static int32_t pipe_blocks(const ias_plan *plan, const ias_csr *A) {
+    const char *e = getenv("IAS_PIPE_BLOCKS");
+    const int32_t nb = e && *e ? (int32_t)atoi(e) : 4;
+    const char *m = getenv("IAS_PIPE_MIN");
+    const int64_t min_entries = m && *m ? (int64_t)atoll(m) : (int64_t)(4 << 20);
+    if (nb <= 1 || plan->serial || A->nnz < min_entries) return 1;
+    return nb;
+}
+
 extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, const ias_csr *B, ias_csr *C,
                                            int32_t order, ias_report *rep) {
     if (!plan || !C) return IAS_ERROR_INVALID_ARGUMENT;
@@ -877,9 +861,11 @@ extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, con
     C->rows = A->rows;
     C->cols = B->cols;
     int64_t nnz = 0;
-    if (onepass_enabled()) {
-        IAS_TRY(plan->onepass_prepare(ra, rb, A->rows, B->cols, A->nnz, rep));
-        const ias_status st = plan->onepass_run(ra, rb, C->row_ptr, C->col, C->val, C->nnz, 0, 0, &nnz, rep);
+    if (pipe_blocks(plan, A) > 1) {
+        // row blocks: each block's symbolic pass overlaps the previous block's
+        // numeric pass (two sub-plans, spgemm_engine.hpp)
+        const ias_status st = plan->pipelined(ra, rb, A->rows, B->cols, A->nnz, C->row_ptr, C->col, C->val,
+                                              C->nnz, pipe_blocks(plan, A), &nnz, rep);
         if (st == IAS_ERROR_INSUFFICIENT_CAPACITY) C->nnz = nnz;
         IAS_TRY(st);
     } else {

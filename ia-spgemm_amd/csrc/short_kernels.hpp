@@ -76,6 +76,8 @@ struct ShortLds {
     int64_t ebs[SH_ENT];         // non-empty entries: B-row start - row-relative first product
     double eav[NUM ? SH_ENT : 1];
     unsigned long long wmask[K];
+    // the numeric pass stages a row's C values (up to P doubles) over minp
+    static_assert(!NUM || sizeof(int32_t) * S >= sizeof(double) * P, "staged C values overflow minp");
 };
 
 __device__ __forceinline__ void sh_wave_sync() {

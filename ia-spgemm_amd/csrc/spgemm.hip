@@ -4,7 +4,6 @@
 // the per-row algorithm and DESIGN.md §4 for the pipeline and its roofline.
 #include <hipcub/hipcub.hpp>
 #include "spgemm_kernels.hpp"
-#include "onepass_kernels.hpp"
 #include "sym2_kernels.hpp"
 #include "sym3_kernels.hpp"
 #include "num2_kernels.hpp"
@@ -1910,8 +1909,10 @@ ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
 
 ias_plan::~ias_plan() {
     hipSetDevice(device);
-    delete sub;
-    sub = nullptr;
+    for (auto &q : pipe) {
+        delete q;
+        q = nullptr;
+    }
     if (stream) hipStreamSynchronize((hipStream_t)stream);
     for (auto &b : bufs)
         if (b.p) hipFree(b.p);
@@ -1930,7 +1931,6 @@ ias_plan::~ias_plan() {
     for (auto &e : n2_ev)
         if (e) hipEventDestroy(e);
     if (host_counters) hipHostFree(host_counters);
-    if (host_info) hipHostFree(host_info);
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
 }
 
@@ -1959,7 +1959,6 @@ ias_status ias_plan::init(int dev, void *strm) {
     const char *e = getenv("IAS_SERIAL");
     serial = e && *e && *e != '0';
     HIPC(hipHostMalloc(&host_counters, 3 * sizeof(Counters)));   // [0], [1]: counters; [2]: A's base
-    HIPC(hipHostMalloc(&host_info, 64));
     return IAS_SUCCESS;
 }
 
@@ -2420,7 +2419,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         k_fill_rows<<<grid_for(rows * WAVE, 256), 256, 0, s>>>(out.ptr, rows, out.row_idx);
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[4], s));
-    if (num_count[part_bin] > 0) {
+    if (num_count[part_bin] > 0 && !defer_checks) {
         int32_t of = 0;
         HIPC(hipMemcpyAsync(&of, &dc2->overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
@@ -2457,179 +2456,182 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
 }
 
 
-// =================================================================== single pass
-// Exclusive scan of n int32 values into out[0..n] (out[n] = total), on `s`.
-static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s) {
-    const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, nullptr);
-    k_scan_partials<<<1, 1024, 0, s>>>(part, nb);
-    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, out);
-}
-
-ias_status ias_plan::onepass_prepare(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
-                                     int64_t a_entries, ias_report *rep) {
-    hipStream_t s = (hipStream_t)stream;
-    HIPC(hipSetDevice(device));
-    IAS_TRY(analysis_launch(A, B, rows, a_entries, true));
-    const size_t rn = (size_t)rows + 2;
-    IAS_TRY(reserve(B_OPCF, sizeof(int32_t) * rn));
-    IAS_TRY(reserve(B_OPBF, sizeof(int32_t) * rn));
-    IAS_TRY(reserve(B_OPCID, sizeof(int64_t) * rn));
-    IAS_TRY(reserve(B_OPBPOS, sizeof(int64_t) * rn));
-    IAS_TRY(reserve(B_OPCROW, sizeof(int64_t) * rn));
-    IAS_TRY(reserve(B_OPSTAT, sizeof(unsigned long long) * rn));
-    IAS_TRY(reserve(B_OPMISC, 256));
-    IAS_TRY(reserve(B_OPBROW, sizeof(int64_t) * rn));
-    IAS_TRY(reserve(B_OPBLEN, sizeof(int32_t) * rn));
-    IAS_TRY(reserve(B_OPBPTR, sizeof(int64_t) * rn));
-    int32_t *cf = as<int32_t>(bufs[B_OPCF]), *bf = as<int32_t>(bufs[B_OPBF]);
-    int64_t *cid = as<int64_t>(bufs[B_OPCID]), *bpos = as<int64_t>(bufs[B_OPBPOS]);
-    int64_t *crow = as<int64_t>(bufs[B_OPCROW]), *brow = as<int64_t>(bufs[B_OPBROW]);
-    int64_t *bptr = as<int64_t>(bufs[B_OPBPTR]);
-    int32_t *blen = as<int32_t>(bufs[B_OPBLEN]);
-    int32_t *misc = as<int32_t>(bufs[B_OPMISC]);   // [0] ticket, [1] nchunks
-    int64_t *part = as<int64_t>(bufs[B_PART]);
-    Counters *dc = as<Counters>(bufs[B_CNT]);
-    Counters *hc = (Counters *)host_counters;
-    int64_t *hi = (int64_t *)host_info;
-    if (rows > 0) {
-        k_op_flags<<<grid_for(rows, 256), 256, 0, s>>>(as<int64_t>(bufs[B_POFF]), as<int32_t>(bufs[B_PROD]), rows,
-                                                       cf, bf);
-        scan_i32(cf, rows, part, cid, s);
-        scan_i32(bf, rows, part, bpos, s);
-        k_op_lists<<<grid_for(rows, 256), 256, 0, s>>>(cf, cid, bf, bpos, rows, crow, misc + 1, brow);
-        k_op_biglen<<<grid_for(rows, 256), 256, 0, s>>>(A, bpos, brow, rows, blen);
-        scan_i32(blen, rows, part, bptr, s);
-        CHECK_LAUNCH("single-pass chunking", s);
-        HIPC(hipMemcpyAsync(hi, bpos + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        HIPC(hipMemcpyAsync(hi + 1, bptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    } else {
-        hi[0] = hi[1] = 0;
-    }
-    HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + A's base entry
-    HIPC(hipStreamSynchronize(s));
-    const Counters c1 = *hc;
-    ax_aval = A.val + (rows > 0 ? c1.a_base : 0);
-    if (c1.overflow) {
-        set_last_error("A's row pointer addresses entries beyond its nnz (%lld)", (long long)a_entries);
-        return IAS_ERROR_INVALID_ARGUMENT;
-    }
-    flops = (int64_t)c1.flops;
-    max_prod = c1.max_prod;
-    op_nbig = hi[0];
-    op_nbe = hi[1];
-    HIPC(hipEventRecord(ev[1], s));
-    if (op_nbig > 0) {
-        IAS_TRY(reserve(B_OPBCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(op_nbe, 1)));
-        IAS_TRY(reserve(B_OPBVAL, sizeof(double) * (size_t)std::max<int64_t>(op_nbe, 1)));
-        k_op_bigcopy<<<(unsigned)op_nbig, 256, 0, s>>>(A, brow, bptr, as<int32_t>(bufs[B_OPBCOL]),
-                                                        as<double>(bufs[B_OPBVAL]));
-        CHECK_LAUNCH("k_op_bigcopy", s);
-        if (!sub) {
-            sub = new ias_plan();
-            IAS_TRY(sub->init(device, stream));
+// =================================================================== row-block pipeline
+namespace ias {
+namespace dev {
+// Products of every row (sum of its entries' B-row lengths, capped at
+// INT32_MAX): one wave per row, the lanes striding its entries.
+__global__ void k_row_cost(Rows A, Rows B, int64_t rows, int32_t *cost) {
+    const int lane = (int)(threadIdx.x & (WAVE - 1));
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
+    const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
+    for (int64_t r = w0; r < rows; r += nw) {
+        const int64_t e0 = A.ptr[r], e1 = A.ptr[r + 1];
+        int64_t t = 0;
+        for (int64_t e = e0 + lane; e < e1; e += WAVE) {
+            int64_t bs;
+            int32_t bn;
+            B.row(A.col[e], bs, bn);
+            t += bn;
         }
-        const Rows ab{bptr, nullptr, 0, as<int32_t>(bufs[B_OPBCOL]), as<double>(bufs[B_OPBVAL])};
-        IAS_TRY(sub->symbolic(ab, B, op_nbig, cols, op_nbe, nullptr));
+        for (int o = WAVE / 2; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        if (lane == 0) cost[r] = (int32_t)(t < 0x7FFFFFFF ? t : 0x7FFFFFFF);
     }
-    HIPC(hipEventRecord(ev[2], s));
-    if (rep) {
-        rep->flops = flops;
-        rep->max_row_products = max_prod;
-    }
-    return IAS_SUCCESS;
 }
+// Block bounds by cost: bounds[b] = the first row whose cost prefix is >=
+// b/NB of the total (binary search over the prefix), plus each bound's A
+// entry offset.
+__global__ void k_row_blocks(const int64_t *ptr, const int64_t *pre, int64_t rows, int32_t nb, int64_t *bounds,
+                             int64_t *ents) {
+    const int b = (int)threadIdx.x;
+    if (b > nb) return;
+    const int64_t tot = pre[rows];
+    int64_t r;
+    if (b == 0) r = 0;
+    else if (b == nb) r = rows;
+    else {
+        const int64_t want = tot * b / nb;
+        int64_t lo = 0, hi = rows;   // first row r with pre[r] >= want
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if (pre[mid] < want) lo = mid + 1;
+            else hi = mid;
+        }
+        r = lo;
+    }
+    bounds[b] = r;
+    ents[b] = ptr[r] - ptr[0];
+}
+// C's row pointer of a block: the block's own (from 0) shifted to its place
+__global__ void k_place_ptr(const int64_t *src, int64_t n, int64_t base, int64_t *dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i] + base;
+}
+}  // namespace dev
+}  // namespace ias
 
-// IAS_OP_WAVES: workgroups per CU of the chunk launch (0 = occupancy).
-ias_status ias_plan::onepass_run(const Rows &A, const Rows &B, int64_t *c_ptr, int32_t *c_col, double *c_val,
-                                 int64_t cap, int32_t order, int32_t first_assign, int64_t *nnz_c,
-                                 ias_report *rep) {
+ias_status ias_plan::pipelined(const Rows &A, const Rows &B, int64_t rows, int64_t cols, int64_t a_entries,
+                               int64_t *c_ptr, int32_t *c_col, double *c_val, int64_t cap, int32_t nb,
+                               int64_t *nnz_c, ias_report *rep) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
-    const int64_t rows = n_rows;
-    int64_t *hi = (int64_t *)host_info;
-    int32_t *misc = as<int32_t>(bufs[B_OPMISC]);
     if (rows <= 0) {
         HIPC(hipMemsetAsync(c_ptr, 0, sizeof(int64_t), s));
         HIPC(hipStreamSynchronize(s));
         *nnz_c = 0;
         return IAS_SUCCESS;
     }
-    HIPC(hipMemsetAsync(bufs[B_OPSTAT].p, 0, sizeof(unsigned long long) * ((size_t)rows + 1), s));
-    HIPC(hipMemsetAsync(misc, 0, sizeof(int32_t), s));
-    OnepassArgs oa{A,
-                   B,
-                   ax_view(),
-                   as<int32_t>(bufs[B_AXR]),
-                   as<int64_t>(bufs[B_AXP]),
-                   as<int64_t>(bufs[B_POFF]),
-                   as<int32_t>(bufs[B_PROD]),
-                   as<int64_t>(bufs[B_OPCROW]),
-                   misc + 1,
-                   op_nbig > 0 ? (const int32_t *)sub->bufs[B_NNZ].p : nullptr,
-                   as<int64_t>(bufs[B_OPBPOS]),
-                   as<unsigned long long>(bufs[B_OPSTAT]),
-                   misc,
-                   c_ptr,
-                   c_col,
-                   c_val,
-                   rows,
-                   cap,
-                   order,
-                   first_assign};
-    auto kern = k_onepass<OP_BLOCK, OP_NPM>;
-    int64_t grid = resident_blocks(kern, OP_BLOCK, 0);
-    grid = std::max<int64_t>(1, std::min<int64_t>(grid, rows));
-    HIPC(hipEventRecord(ev[5], s));
-    kern<<<(unsigned)grid, OP_BLOCK, 0, s>>>(oa);
-    HIPC(hipEventRecord(ev[6], s));
-    CHECK_LAUNCH("k_onepass", s);
-    HIPC(hipMemcpyAsync(hi + 2, c_ptr + rows, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    nb = (int32_t)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nb, rows, 64}));
+    for (auto &q : pipe)
+        if (!q) {
+            q = new ias_plan();
+            const ias_status st = q->init(device, nullptr);
+            if (st != IAS_SUCCESS) {
+                delete q;
+                q = nullptr;
+                return st;
+            }
+            q->defer_checks = true;  // no host wait inside numeric(): checked at the end
+        }
+    {
+        // IAS_PIPE_SERIAL=1: one stream per sub-plan (no side streams inside a block)
+        const char *e = getenv("IAS_PIPE_SERIAL");
+        const bool ser = e && *e == '1';
+        for (auto q : pipe) q->serial = ser;
+    }
+    HIPC(hipEventRecord(ev[0], s));
+    for (auto q : pipe) HIPC(hipStreamWaitEvent((hipStream_t)q->stream, ev[0], 0));   // after the caller's work
+    // blocks of equal products (R-MAT's low rows hold most of them: blocks of
+    // equal A entries were measured 1.2 ms slower per K3' step than one block)
+    IAS_TRY(reserve(B_TMP0, sizeof(int64_t) * 2 * (size_t)(nb + 1)));
+    IAS_TRY(reserve(B_TMP1, sizeof(int32_t) * (size_t)(rows + 1)));
+    IAS_TRY(reserve(B_TMP2, sizeof(int64_t) * (size_t)(rows + 1)));
+    IAS_TRY(reserve(B_PART, sizeof(int64_t) * (size_t)((rows + SCAN_TILE - 1) / SCAN_TILE + 4)));
+    int64_t *bnd = as<int64_t>(bufs[B_TMP0]), *pre = as<int64_t>(bufs[B_TMP2]);
+    dev::k_row_cost<<<(unsigned)std::min<int64_t>(grid_for(rows * WAVE, 256), 8192), 256, 0, s>>>(
+        A, B, rows, as<int32_t>(bufs[B_TMP1]));
+    scan_i32(as<int32_t>(bufs[B_TMP1]), rows, as<int64_t>(bufs[B_PART]), pre, s);
+    dev::k_row_blocks<<<1, 128, 0, s>>>(A.ptr, pre, rows, nb, bnd, bnd + nb + 1);
+    std::vector<int64_t> hb(2 * (size_t)(nb + 1));
+    HIPC(hipMemcpyAsync(hb.data(), bnd, sizeof(int64_t) * hb.size(), hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));
-    nnz_total = hi[2];
-    *nnz_c = nnz_total;
-    if (nnz_total > cap) {
-        set_last_error("C needs %lld entries, capacity %lld", (long long)nnz_total, (long long)cap);
+    const int64_t *rb = hb.data(), *eb = hb.data() + nb + 1;
+    int64_t base = 0, fl = 0, mp = 0, mn = 0;
+    bool over = false;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    for (int b = 0; b < nb; ++b) {
+        const int64_t r0 = rb[b], r1 = rb[b + 1];
+        if (r1 <= r0) continue;
+        ias_plan *P = pipe[b & 1];
+        Rows Ab = A;
+        Ab.ptr = A.ptr + r0;   // a row view: entries addressed absolutely
+        IAS_TRY(P->symbolic(Ab, B, r1 - r0, cols, eb[b + 1] - eb[b], nullptr));
+        fl += P->flops;
+        mp = std::max<int64_t>(mp, P->max_prod);
+        mn = std::max<int64_t>(mn, P->max_nnz);
+        const int64_t nb_nnz = P->nnz_total;
+        hipStream_t t = (hipStream_t)P->stream;
+        if (base + nb_nnz > cap) over = true;
+        // the row pointer is written in full even past the capacity (ias.h)
+        dev::k_place_ptr<<<grid_for(r1 - r0 + 1, 256), 256, 0, t>>>(as<int64_t>(P->bufs[B_PTR]), r1 - r0 + 1,
+                                                                  base, c_ptr + r0);
+        done[b & 1] = P->ev[7];
+        HIPC(hipEventRecord(P->ev[7], t));
+        if (!over) {
+            const Out out{c_ptr + r0, 0, c_col, c_val, nullptr, 0, 0, nullptr};
+            IAS_TRY(P->numeric(Ab, B, out, nullptr));
+            HIPC(hipEventRecord(P->ev[7], t));
+        }
+        base += nb_nnz;
+    }
+    // the plan stream (the caller's) waits for both sub-plans
+    for (auto e : done)
+        if (e) HIPC(hipStreamWaitEvent(s, e, 0));
+    // the partitioned numeric pass's table overflow (deferred in the sub-plans)
+    for (auto q : pipe) {
+        int32_t of = 0;
+        HIPC(hipMemcpyAsync(&of, &(as<Counters>(q->bufs[B_CNT]) + 1)->overflow, sizeof(int32_t),
+                            hipMemcpyDeviceToHost, (hipStream_t)q->stream));
+        HIPC(hipStreamSynchronize((hipStream_t)q->stream));
+        if (of) {
+            set_last_error("hash partition table overflow in the numeric pass");
+            return IAS_ERROR_OVERFLOW;
+        }
+    }
+    if (over) {
+        // row pointer only: C's entries need more than its capacity
+        HIPC(hipStreamSynchronize(s));
+        *nnz_c = base;
+        set_last_error("C needs %lld entries, capacity %lld", (long long)base, (long long)cap);
         return IAS_ERROR_INSUFFICIENT_CAPACITY;
     }
-    if (op_nbig > 0) {
-        IAS_TRY(reserve(B_OPBCPTR, sizeof(int64_t) * ((size_t)op_nbig + 1)));
-        int64_t *bcptr = as<int64_t>(bufs[B_OPBCPTR]);
-        k_op_bigptr<<<grid_for(op_nbig, 256), 256, 0, s>>>(c_ptr, as<int64_t>(bufs[B_OPBROW]), op_nbig, bcptr);
-        const Rows ab{as<int64_t>(bufs[B_OPBPTR]), nullptr, 0, as<int32_t>(bufs[B_OPBCOL]),
-                      as<double>(bufs[B_OPBVAL])};
-        const Out out{bcptr, 0, c_col, c_val, nullptr, order, first_assign, nullptr};
-        IAS_TRY(sub->numeric(ab, B, out, nullptr));
-    }
     HIPC(hipEventRecord(ev[4], s));
+    *nnz_c = base;
+    nnz_total = base;
+    flops = fl;
+    max_prod = (int32_t)mp;
+    max_nnz = (int32_t)mn;
+    n_rows = rows;
     if (rep) {
-        HIPC(hipMemsetAsync(misc + 2, 0, sizeof(int32_t), s));
-        k_op_maxlen<<<grid_for(rows, 256), 256, 0, s>>>(c_ptr, rows, misc + 2);
-        HIPC(hipMemcpyAsync((int32_t *)(hi + 3), misc + 2, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    }
-    HIPC(hipStreamSynchronize(s));
-    if (rep) {
-        max_nnz = *(int32_t *)(hi + 3);
-        rep->max_row_nnz = max_nnz;
-        float a = 0, b = 0, n = 0, t = 0, f = 0;
-        hipEventElapsedTime(&a, ev[0], ev[1]);
-        hipEventElapsedTime(&b, ev[1], ev[2]);
-        hipEventElapsedTime(&n, ev[2], ev[4]);
+        HIPC(hipEventSynchronize(ev[4]));
+        float t = 0;
         hipEventElapsedTime(&t, ev[0], ev[4]);
-        hipEventElapsedTime(&f, ev[5], ev[6]);
-        rep->ms_analysis = a;
-        rep->ms_symbolic = b;
-        rep->ms_numeric = n;
         rep->ms_total = t;
-        rep->ms_stream = f;
-        rep->flops = flops;
-        rep->nnz_c = nnz_total;
-        rep->max_row_products = max_prod;
-        rep->stream_products = flops - (op_nbig > 0 ? sub->flops : 0);
-        rep->stream_nnz = nnz_total - (op_nbig > 0 ? sub->nnz_total : 0);
+        rep->flops = fl;
+        rep->nnz_c = base;
+        rep->max_row_products = mp;
+        rep->max_row_nnz = mn;
     }
     return IAS_SUCCESS;
+}
+
+// =================================================================== scan
+// Exclusive scan of n int32 values into out[0..n] (out[n] = total), on `s`.
+static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s) {
+    const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, nullptr);
+    k_scan_partials<<<1, 1024, 0, s>>>(part, nb);
+    k_scan_apply<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(in, n, part, out);
 }
 
 // ------------------------------------------------------------------ row sort host

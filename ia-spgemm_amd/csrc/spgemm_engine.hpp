@@ -63,9 +63,6 @@ struct ias_plan {
         B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5,
-        // single-pass path (onepass)
-        B_OPCF, B_OPBF, B_OPCID, B_OPBPOS, B_OPCROW, B_OPSTAT, B_OPMISC, B_OPBROW, B_OPBLEN, B_OPBPTR,
-        B_OPBCOL, B_OPBVAL, B_OPBCPTR,
         // partition buckets of the symbolic pass
         B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
         // work units of the row-unit numeric pass (num2)
@@ -92,6 +89,7 @@ struct ias_plan {
     ias_status fork();
     ias_status join();
     bool serial = false;   // IAS_SERIAL=1: everything on `stream` (per-kernel profiling)
+    bool defer_checks = false;   // numeric(): no host wait for the overflow flag (pipeline sub-plans)
     // small products (flops < SMALL_FLOPS): the bins run on `stream` too — a
     // fork / join across queues costs ~30 us of event latency each, more than
     // the bins of a small product overlap
@@ -130,22 +128,15 @@ struct ias_plan {
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                         int64_t cols, int64_t a_entries, ias_report *rep);
     ias::dev::AxView ax_view();
-    // Single pass (csrc/onepass_kernels.hpp): C = A*B into caller arrays of
-    // capacity >= flops(A*B); rows with many products go through the two-phase
-    // engine of `sub` (symbolic before, numeric after the chunk launch).
-    // Sets *nnz_c; order/first_assign as ias::dev::Out.
-    // prepare: analysis, chunking, big-row symbolic (sets flops); run: the
-    // chunk launch + big-row numeric into C of capacity `cap` — when nnz(C)
-    // exceeds it nothing is written beyond, *nnz_c says what is needed and
-    // IAS_ERROR_INSUFFICIENT_CAPACITY is returned (C's row pointer is valid).
-    ias_status onepass_prepare(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
-                               int64_t cols, int64_t a_entries, ias_report *rep);
-    ias_status onepass_run(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t *c_ptr, int32_t *c_col,
-                           double *c_val, int64_t cap, int32_t order, int32_t first_assign, int64_t *nnz_c,
-                           ias_report *rep);
-    ias_plan *sub = nullptr;      // big rows of the single-pass path (two-phase engine)
-    int64_t op_nbig = 0, op_nbe = 0;
-    void *host_info = nullptr;    // pinned scalars of the single-pass path
+    // Row-block pipeline (ias_csr_mul_csr_into, one call): A's rows in blocks,
+    // each block's symbolic pass on one of two sub-plans (own stream, serial)
+    // while the previous block's numeric pass runs on the other.  Sets
+    // *nnz_c; IAS_ERROR_INSUFFICIENT_CAPACITY when C's capacity is exceeded
+    // (nothing written beyond it, *nnz_c = what is needed).
+    ias_plan *pipe[2] = {nullptr, nullptr};
+    ias_status pipelined(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows, int64_t cols,
+                         int64_t a_entries, int64_t *c_ptr, int32_t *c_col, double *c_val, int64_t cap,
+                         int32_t nblocks, int64_t *nnz_c, ias_report *rep);
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
 };

@@ -1,6 +1,7 @@
 """Full-size parity on the GPU: the BASELINE.json configurations K1, K2, K3'
 and K3 through the device-resident two-phase C-ABI
-(ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute), checked against the
+(ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, and the one-call row-block
+pipeline ias_csr_mul_csr_into), checked against the
 oracle's CSR_MUL_CSR restatement recorded in tests/golden/generator_stats.json
 by make_generator_stats.py:
 
@@ -44,8 +45,12 @@ def make(rec):
     return {"rmat": ias.gen_rmat, "band": ias.gen_band, "ell": ias.gen_ell}[rec["kind"]](*rec["args"])
 
 
-def device_spgemm(torch, A, order=ias.ORDER_REFERENCE):
-    """C = A*A with A and C in HBM; returns (row_ptr, col, val) torch tensors and the report."""
+def device_spgemm(torch, A, order=ias.ORDER_REFERENCE, via="twophase"):
+    """C = A*A with A and C in HBM; returns (row_ptr, col, val) torch tensors and
+    the symbolic report.  via="twophase": ias_csr_mul_csr_nnz + _compute;
+    via="into": one ias_csr_mul_csr_into call into C of capacity flops(A*A)
+    (the row-block pipeline for large A, each block's symbolic pass beside the
+    previous block's numeric pass)."""
     dev = torch.device("cuda", 0)
     rp = torch.from_numpy(A.row_ptr).to(dev)
     ci = torch.from_numpy(A.col).to(dev)
@@ -65,12 +70,18 @@ def device_spgemm(torch, A, order=ias.ORDER_REFERENCE):
         ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Am), C.byref(n), None, C.byref(rs)),
                   "nnz")
         nnz = int(n.value)
+        cap = nnz if via == "twophase" else int(rs.flops)
         c_rp = torch.empty(A.rows + 1, dtype=torch.int64, device=dev)
-        c_ci = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
-        c_va = torch.empty(max(nnz, 1), dtype=torch.float64, device=dev)
-        Cm = csr(c_rp, c_ci, c_va, A.rows, nnz)
-        ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Am), C.byref(Cm), order,
-                                                  C.byref(rep)), "compute")
+        c_ci = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+        c_va = torch.empty(max(cap, 1), dtype=torch.float64, device=dev)
+        Cm = csr(c_rp, c_ci, c_va, A.rows, cap)
+        if via == "twophase":
+            ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Am), C.byref(Cm), order,
+                                                      C.byref(rep)), "compute")
+        else:
+            ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Am), C.byref(Cm), order,
+                                                   C.byref(rep)), "into")
+            assert Cm.nnz == nnz, (Cm.nnz, nnz)
         torch.cuda.synchronize()
     finally:
         ias.lib.ias_plan_destroy(plan)
@@ -82,13 +93,14 @@ def rows_block(A, r0, r1):
     return ob.Mat(r1 - r0, A.cols, A.row_ptr[r0:r1 + 1] - s, A.col[s:e], A.val[s:e])
 
 
+@pytest.mark.parametrize("via", ["twophase", "into"])
 @pytest.mark.parametrize("name", CASES)
-def test_fullsize_against_oracle(torch_dev, name):
+def test_fullsize_against_oracle(torch_dev, name, via):
     torch = torch_dev
     rec = STATS[name]
     A = make(rec)
     assert A.nnz == rec["nnz"]
-    c_rp, c_ci, c_va, rs = device_spgemm(torch, A)
+    c_rp, c_ci, c_va, rs = device_spgemm(torch, A, via=via)
     try:
         assert rs.flops == rec["flops"]
         rp = c_rp.cpu().numpy()

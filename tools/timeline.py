@@ -1,36 +1,50 @@
 #!/usr/bin/env python3
-"""Timeline of one pipeline run from a rocprofv3 --kernel-trace CSV: kernels
-of the LAST occurrence of the anchor kernel's run (default k_an_entries, the
-first kernel of analysis), with start / end offsets in us and the gaps
-between kernels (host syncs show up as gaps).
-
-usage: tools/timeline.py <kernel_trace.csv> [anchor]"""
+"""Timeline of one step from a rocprofv3 --kernel-trace CSV: each kernel's
+start / end (us from the step's first kernel), queue and stream, plus the
+busy time (union of kernel intervals) vs the step's span.
+usage: timeline.py run_kernel_trace.csv MARKER [occurrence] [max_rows]
+MARKER is a kernel-name substring that starts a step (e.g. k_row_blocks)."""
 import csv
 import re
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-anchor = sys.argv[2] if len(sys.argv) > 2 else "k_an_entries"
-rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-
 
 def short(n):
-    n = re.sub(r"ias::dev::", "", n)
-    n = re.sub(r"\(.*", "", n).replace("void ", "")
-    return n
+    n = re.sub(r"\(.*$", "", n)
+    n = re.sub(r"^void ", "", n)
+    return n[:70]
 
 
-idx = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
-if len(idx) < 2:
-    sys.exit("anchor %s found %d times" % (anchor, len(idx)))
-lo, hi = idx[-2], idx[-1]
-t0 = int(rows[lo]["Start_Timestamp"])
-busy_end = t0
-for r in rows[lo:hi]:
-    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    gap = (s - busy_end) / 1e3
-    print("%9.1f %9.1f %8.1f  q%-3s %s%s" % ((s - t0) / 1e3, (e - t0) / 1e3, (e - s) / 1e3, r["Queue_Id"],
-                                            short(r["Kernel_Name"])[:56],
-                                            ("   <gap %.1f us>" % gap) if gap > 5 else ""))
-    busy_end = max(busy_end, e)
-print("span %.1f us" % ((busy_end - t0) / 1e3))
+def main():
+    path, marker = sys.argv[1], sys.argv[2]
+    occ = int(sys.argv[3]) if len(sys.argv) > 3 else -1
+    maxr = int(sys.argv[4]) if len(sys.argv) > 4 else 400
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    starts = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
+    i0 = starts[occ]
+    nxt = [i for i in starts if i > i0]
+    i1 = nxt[0] if nxt else len(rows)
+    step = rows[i0:i1]
+    t0 = int(step[0]["Start_Timestamp"])
+    iv = []
+    for r in step[:maxr]:
+        s, e = int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0
+        iv.append((s, e))
+        print(f"{s/1e3:9.1f} {e/1e3:9.1f} {(e-s)/1e3:8.1f}  q{r['Queue_Id']:>2} s{r['Stream_Id']:>2}  {short(r['Kernel_Name'])}")
+    iv = sorted((int(r["Start_Timestamp"]) - t0, int(r["End_Timestamp"]) - t0) for r in step)
+    busy, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    busy += cur_e - cur_s
+    span = max(e for _, e in iv)
+    print(f"kernels {len(step)}  span {span/1e6:.3f} ms  busy {busy/1e6:.3f} ms  idle {(span-busy)/1e6:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
