@@ -5,12 +5,10 @@ Contract:
   python bench.py --gpus N --steps K --warmup W
 One step = one full C = A*A of this rank's row block through the C-ABI,
 inputs resident in HBM, C written into preallocated device arrays.  Default
-`--engine pipe`: one ias_csr_mul_csr_into call per step (C's capacity =
-flops(A*A) >= nnz(C)), the library's row-block pipeline — A's rows in 4
-blocks, each block's symbolic pass beside the previous block's numeric pass.
 `--engine twophase`: ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, as
 cuSPARSE's csrgemmNnz + csrgemm (row analysis, binning, symbolic, scan, host
-read of nnz, numeric + write C).
+read of nnz, numeric + write C).  `--engine into`: one ias_csr_mul_csr_into
+call per step into C of capacity flops(A*A) >= nnz(C).
 
 Workload (default `--config auto`): R-MAT power-law, a,b,c = .45,.15,.15.
 N=1: the north-star headline matrix K3' (2^20 rows, edge factor 20, seed 2;
@@ -63,10 +61,9 @@ def parse(argv=None):
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
-    p.add_argument("--engine", default="pipe", choices=["pipe", "twophase"],
-                   help="pipe: one ias_csr_mul_csr_into call per step (row blocks, each block's symbolic "
-                        "pass overlapping the previous block's numeric pass); twophase: ias_csr_mul_csr_nnz + "
-                        "ias_csr_mul_csr_compute")
+    p.add_argument("--engine", default="twophase", choices=["twophase", "into"],
+                   help="twophase: ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute; into: one "
+                        "ias_csr_mul_csr_into call per step")
     p.add_argument("--no-host-e2e", action="store_true",
                    help="skip the one PCIe-inclusive call with host operands (N=1 only)")
     p.add_argument("--as-rank", default=None,
@@ -220,7 +217,7 @@ def main(argv=None):
         rep = ias.Report()
         rep_s = ias.Report()
 
-        def step_pipe():
+        def step_into():
             Cm.nnz = cap
             ias.check(ias.lib.ias_csr_mul_csr_into(plan, C.byref(Am), C.byref(Bm), C.byref(Cm), order,
                                                    C.byref(rep)), "into")
@@ -236,7 +233,7 @@ def main(argv=None):
             rep.ms_analysis, rep.ms_symbolic = rep_s.ms_analysis, rep_s.ms_symbolic
             return rep
 
-        step = step_pipe if args.engine == "pipe" else step_twophase
+        step = step_into if args.engine == "into" else step_twophase
 
         for _ in range(args.warmup):
             step()
@@ -254,16 +251,7 @@ def main(argv=None):
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        local_nnz = int(Cm.nnz) if args.engine == "pipe" else cap
-        if args.engine == "pipe":
-            # phases and the dominant kernel's event timing come from two-phase
-            # steps after the timed loop (one call per step leaves no phase
-            # boundary: symbolic and numeric blocks overlap)
-            reps = []
-            for _ in range(2):
-                r = step_twophase()
-                reps.append((r.ms_total, r.ms_analysis, r.ms_symbolic, r.ms_numeric, r.ms_stream))
-            Cm.nnz = local_nnz
+        local_nnz = int(Cm.nnz) if args.engine == "into" else cap
         t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         nnz_tot = torch.tensor([float(local_nnz)], dtype=torch.float64, device=dev)
         num_ms = torch.tensor([statistics.mean(x[3] for x in reps)], dtype=torch.float64, device=dev)
@@ -377,7 +365,7 @@ def main(argv=None):
         if as_ranks is not None:
             out["as_rank"] = {"rank": shard, "of": world_req, "rows": [r0, r1],
                               "note": "one rank's shard only: value / nnz_per_s are per-rank figures"}
-            shard_flops = int(rep_s.flops) if args.engine in ("twophase", "pipe") else int(rep.flops)
+            shard_flops = int(rep_s.flops) if args.engine == "twophase" else int(rep.flops)
             out["as_rank"]["flops"] = shard_flops
             out["as_rank"]["nnz_c"] = local_nnz
             out["value"] = round(2.0 * shard_flops / (ms_step * 1e6), 3)

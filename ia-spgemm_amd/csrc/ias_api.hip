@@ -828,20 +828,6 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
     return IAS_SUCCESS;
 }
 
-// Row blocks of the one-call pipeline (IAS_PIPE_BLOCKS, default 4; 1 = off):
-// only for products big enough that a block keeps the GPU busy (A with at
-// least IAS_PIPE_MIN entries, default 4M — the knob lets the parity tests run
-// small inputs through it), and never in the plan's serial (profiling) mode.
-// Read per call (one getenv each: the tests switch them between cases).
-static int32_t pipe_blocks(const ias_plan *plan, const ias_csr *A) {
-    const char *e = getenv("IAS_PIPE_BLOCKS");
-    const int32_t nb = e && *e ? (int32_t)atoi(e) : 4;
-    const char *m = getenv("IAS_PIPE_MIN");
-    const int64_t min_entries = m && *m ? (int64_t)atoll(m) : (int64_t)(4 << 20);
-    if (nb <= 1 || plan->serial || A->nnz < min_entries) return 1;
-    return nb;
-}
-
 extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, const ias_csr *B, ias_csr *C,
                                            int32_t order, ias_report *rep) {
     if (!plan || !C) return IAS_ERROR_INVALID_ARGUMENT;
@@ -861,28 +847,19 @@ extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, con
     C->rows = A->rows;
     C->cols = B->cols;
     int64_t nnz = 0;
-    if (pipe_blocks(plan, A) > 1) {
-        // row blocks: each block's symbolic pass overlaps the previous block's
-        // numeric pass (two sub-plans, spgemm_engine.hpp)
-        const ias_status st = plan->pipelined(ra, rb, A->rows, B->cols, A->nnz, C->row_ptr, C->col, C->val,
-                                              C->nnz, pipe_blocks(plan, A), &nnz, rep);
-        if (st == IAS_ERROR_INSUFFICIENT_CAPACITY) C->nnz = nnz;
-        IAS_TRY(st);
-    } else {
-        // two-phase engine behind the same call: nnz, then values when they fit
-        IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
-        nnz = plan->nnz_total;
-        HIPC(hipMemcpyAsync(C->row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
-                            hipMemcpyDeviceToDevice, s));
-        if (nnz > C->nnz) {
-            HIPC(hipStreamSynchronize(s));
-            set_last_error("C needs %lld entries, capacity %lld", (long long)nnz, (long long)C->nnz);
-            C->nnz = nnz;
-            return IAS_ERROR_INSUFFICIENT_CAPACITY;
-        }
-        dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0, nullptr};
-        IAS_TRY(plan->numeric(ra, rb, out, rep));
+    // the two-phase engine behind one call: nnz, then values when they fit
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
+    nnz = plan->nnz_total;
+    HIPC(hipMemcpyAsync(C->row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
+                        hipMemcpyDeviceToDevice, s));
+    if (nnz > C->nnz) {
+        HIPC(hipStreamSynchronize(s));
+        set_last_error("C needs %lld entries, capacity %lld", (long long)nnz, (long long)C->nnz);
+        C->nnz = nnz;
+        return IAS_ERROR_INSUFFICIENT_CAPACITY;
     }
+    dev::Out out{C->row_ptr, 0, C->col, C->val, nullptr, 0, 0, nullptr};
+    IAS_TRY(plan->numeric(ra, rb, out, rep));
     C->nnz = nnz;
     if (order == IAS_ORDER_SORTED)
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, 0));

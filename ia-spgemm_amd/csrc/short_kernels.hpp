@@ -30,24 +30,11 @@ namespace ias {
 namespace dev {
 
 constexpr int SH_WPB = 4;   // waves (rows) per workgroup
-#ifndef SH_ST_EARLY
-#define SH_ST_EARLY 1   // numeric: C's row start loaded with the row's A entries
-#endif
-#ifndef SH_SYM_SF12
-#define SH_SYM_SF12 2   // A/B knobs: symbolic slots for K = 1, 2 rows; numeric for K = 4
-#endif
-#ifndef SH_NUM_SF4
-#define SH_NUM_SF4 2
-#endif
-#ifndef SH_SYM_SF4
-#define SH_SYM_SF4 4   // symbolic table slots per product bound, K = 4 rows
-#endif
-#ifndef SH_NODUP
-#define SH_NODUP 1   // numeric: rows without duplicates written straight from the gather
-#endif
-#ifndef SH_STAGE
-#define SH_STAGE 1   // numeric: C staged in LDS, 16-byte stores
-#endif
+// table slots per product bound: symbolic K = 1, 2 rows; numeric K = 4 rows;
+// symbolic K = 4 rows
+constexpr int SH_SYM_SF12 = 2;
+constexpr int SH_NUM_SF4 = 2;
+constexpr int SH_SYM_SF4 = 4;
 typedef int32_t sh_i32x4 __attribute__((ext_vector_type(4)));
 typedef double sh_f64x2 __attribute__((ext_vector_type(2)));
 constexpr int SH_ENT = 64;  // A entries per short row at most (the sym2 bins hold 8 * entries <= bound)
@@ -186,10 +173,7 @@ __device__ __forceinline__ int sh_insert(int32_t *keys, const int32_t (&c)[K], u
 // Rows with more duplicates than this take the table path (dupn -1: the
 // numeric LDS value / direct-write bins), which adds them in parallel; the
 // short numeric pass adds duplicates one at a time.
-#ifndef SH_DUP_MAX_DEF
-#define SH_DUP_MAX_DEF 8   // K1 numeric 0.097 vs 0.103 ms with 16 (32: 0.103); K3' within noise
-#endif
-constexpr int SH_DUP_MAX = SH_DUP_MAX_DEF;
+constexpr int SH_DUP_MAX = 8;   // K1 numeric 0.097 vs 0.103 ms with 16 (32: 0.103); K3' within noise
 
 // Persistent waves (grid-stride over the bin's rows); the next row's list
 // entry and A entries are loaded while this row is resolved.
@@ -356,9 +340,7 @@ __device__ __forceinline__ double sh_readlane(double v, int l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
-#ifndef SH_NUM_WPE
-#define SH_NUM_WPE 1   // minimum waves per SIMD the register allocation must allow (A/B knob)
-#endif
+constexpr int SH_NUM_WPE = 1; // minimum waves per SIMD the register allocation must allow (A/B knob)
 template <int K>
 __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_NUM_WPE))) void k_short_num(ShortArgs a, Out out) {
     using LDS = ShortLds<K, true>;
@@ -378,32 +360,22 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
     ShEnt en = sh_load<true>(a, ref, true);
     // C's row start is loaded with the row's A entries (not after the table
     // work: one dependent global load less per row)
-#if SH_ST_EARLY
     int64_t st = out.start(ref.row);
-#endif
     int32_t rn = out.len[ref.row];   // the row's nnz (symbolic pass)
     RowRef nref = sh_ref(a, idx + stride);
     while (idx < a.count) {
         const bool nvalid = idx + stride < a.count;
         const ShEnt nen = sh_load<true>(a, nref, nvalid);
         const int32_t nrn = nvalid ? out.len[nref.row] : 0;
-#if SH_ST_EARLY
         const int64_t nst = nvalid ? out.start(nref.row) : 0;
-#else
-        const int64_t st = out.start(ref.row);
-#endif
         const RowRef nnref = sh_ref(a, idx + 2 * stride);
         int32_t c[K];
         double pv[K];
         const int32_t P = short_gather<K, true>(a, L, en, c, pv);
-#if SH_NODUP
         if (rn == P) {
             // no duplicates (nnz = products): every product is its column's
             // first touch, rank = product index — C is the products in reverse
             // (forward for COO) order, each 0.0 + a*b (a*b); no table
-#if !SH_ST_EARLY
-            const int64_t st = out.start(ref.row);
-#endif
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (c[k] != SH_EMPTY) {
@@ -415,14 +387,11 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
             ref = nref;
             en = nen;
             rn = nrn;
-#if SH_ST_EARLY
             st = nst;
-#endif
             nref = nnref;
             idx += stride;
             continue;
         }
-#endif
         uint32_t slot[K];
         sh_insert<LDS::S, K>(L.keys, c, slot);
 #pragma unroll
@@ -443,14 +412,6 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
             if (ft[k] && !out.first_assign) pv[k] = 0.0 + pv[k];
         }
         sh_wave_sync();   // every lane has read the table
-#if !SH_STAGE
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (c[k] != SH_EMPTY) {   // the table empty for the next row
-                L.keys[slot[k]] = SH_EMPTY;
-                L.minp[slot[k]] = 0x7FFFFFFF;
-            }
-#endif
         // duplicates (at most SH_DUP_MAX): added to their first touch's
         // register, one at a time in product order
 #pragma unroll
@@ -470,7 +431,6 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
                     }
             }
         }
-#if SH_STAGE
         // The row's C entries staged by position in the table's LDS (no longer
         // needed: the next row re-initialises it) and written as ascending
         // 16-byte pieces aligned to the destination (4 columns / 2 values per
@@ -519,25 +479,10 @@ __global__ __launch_bounds__(64 * SH_WPB) __attribute__((amdgpu_waves_per_eu(SH_
             }
             sh_wave_sync();
         }
-#else
-        // C: position start + nnz-1-rank (reverse first touch) or start + rank;
-        // a window's first touches are consecutive ranks, so each store is one
-        // contiguous (descending) run
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (ft[k]) {
-                const int64_t pos = st + (out.order == 0 ? nft - 1 - rk[k] : rk[k]);
-                __builtin_nontemporal_store(c[k], &out.col[pos]);
-                __builtin_nontemporal_store(pv[k], &out.val[pos]);
-            }
-        sh_wave_sync();
-#endif
         ref = nref;
         en = nen;
         rn = nrn;
-#if SH_ST_EARLY
         st = nst;
-#endif
         nref = nnref;
         idx += stride;
     }

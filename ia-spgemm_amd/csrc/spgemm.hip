@@ -149,8 +149,7 @@ __device__ __forceinline__ void count_bins(const BinSpec &sp, const int (&b)[R],
 }
 
 // ---------------------------------------------------------------- analysis
-// Three passes, all load-balanced: the row of every stored A entry (CSR:
-// AN_FILL lanes per row), then flat over A entries the expanded A (B-row start and
+// Two passes, load-balanced: flat over A entries the expanded A (B-row start and
 // length, A value) — independent of how entries spread over rows, so R-MAT
 // hub rows do not serialise a block — and, after the scan of the B-row
 // lengths, per row: products (GetFlop per row, csr/common_csr.h:290-304) =
@@ -159,24 +158,8 @@ __device__ __forceinline__ void count_bins(const BinSpec &sp, const int (&b)[R],
 constexpr int AN_BLOCK = 256;
 constexpr int AN_U = 4;   // entries per thread in flight
 
-constexpr int AN_FILL = 16;   // lanes per row of k_an_rowfill
-__global__ void k_an_rowfill(Rows A, int64_t rows, int64_t a_entries, int32_t *axr, Counters *cnt) {
-    const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / AN_FILL;
-    const int lane = threadIdx.x & (AN_FILL - 1);
-    if (r >= rows) return;
-    int64_t s;
-    int32_t n;
-    A.row(r, s, n);
-    const int64_t q0 = s - A.base();
-    if (q0 < 0 || q0 + n > a_entries) {
-        if (lane == 0) cnt->overflow = 1;   // row pointer disagrees with the declared entry count
-        return;
-    }
-    for (int32_t i = lane; i < n; i += AN_FILL) axr[q0 + i] = (int32_t)r;
-}
-
-// Expanded A, flat over entries.  CSR: rows from k_an_rowfill; ELL (A.ptr
-// null): row = q / stride, padding entries (beyond len[row]) get no products.
+// Expanded A, flat over entries (ELL, A.ptr null: padding entries beyond
+// len[row] get no products).
 __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t a_entries, AxOut ax) {
     const int64_t abase = A.base();
     const int64_t step = (int64_t)gridDim.x * AN_BLOCK * AN_U;
@@ -215,23 +198,17 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
             ax.bstart[q] = bs[u];
             ax.blen[q] = bn[u];
             if (ax.aval) ax.aval[q] = av[u];
-            if (!A.ptr) ax.row[q] = (int32_t)(q / A.stride);
         }
     }
 }
 
 constexpr int BIN_BLOCK = 256;
-#ifndef BIN_RPT_DEF
-#define BIN_RPT_DEF 8
-#endif
-constexpr int BIN_RPT = BIN_RPT_DEF;             // rows per thread of the row passes
+constexpr int BIN_RPT = 8;   // rows per thread of the row passes
 constexpr int BIN_ROWS = BIN_BLOCK * BIN_RPT;    // rows per block
 // Small row counts use BIN_RPT / 2 rows per thread (twice the blocks: K1's
 // 256k rows 128 -> 256 blocks; its binning 0.354 -> 0.337 ms per step); from
 // BIN_RPT_BIG_ROWS rows on BIN_RPT (K2 / K3': 4 measured 1 % slower).
-#ifndef BIN_RPT_BIG_ROWS
-#define BIN_RPT_BIG_ROWS (1 << 20)
-#endif
+constexpr int BIN_RPT_BIG_ROWS = (1 << 20);
 constexpr int BIN_RPT_SMALL = BIN_RPT > 1 ? BIN_RPT / 2 : 1;
 #define BIN_LAUNCH(kern, nrows, strm, ...)                                                                       \
     do {                                                                                                         \
@@ -462,11 +439,6 @@ template <int SEG, bool NUMERIC>
 __host__ __device__ constexpr size_t team_fixed_bytes() {
     return round16(sizeof(Seg<SEG, NUMERIC>)) + 256;   // segment + 64-int scratch
 }
-// bytes of one team's region: [table(s) | row arrays | segment | scratch]
-// [keys | minp | bits | word prefixes | duplicate (product, target) pairs | scratch]
-__host__ __device__ constexpr size_t sym_team_bytes(uint32_t S, uint32_t W, uint32_t D) {
-    return 2 * round16(4ull * S) + 2 * round16(4ull * W) + round16(8ull * D) + 256;
-}
 template <int SEG>
 __host__ __device__ constexpr size_t val_team_bytes(uint32_t S) {
     return round16(8ull * S) + 2 * round16(4ull * S) + team_fixed_bytes<SEG, true>();
@@ -479,86 +451,6 @@ __host__ __device__ constexpr size_t dw_team_bytes(uint32_t S) {
 __device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_t count) {
     if (idx < count) return list[idx];
     return RowRef{0, -1, 0};
-}
-
-// Symbolic pass of the LDS bins: distinct columns (nnz_row), the row's
-// first-touch bitmap with per-word prefix counts, and its duplicate list
-// (dupn[row] = its length, or -1 when it exceeded dcap: the row then takes
-// the table path in the numeric pass).  LDS per team:
-// [keys 4S | minp 4S | bits 4W | dup targets 4D | scratch].
-// Teams walk rows idx, idx + nteams, ... (one row each when the grid covers
-// the list); the next row's list entry and first columns are loaded while
-// the current row is hashed.  WPE: minimum waves per SIMD the register
-// allocation must allow (1: none).
-template <int TEAM, int K, int TPW, int WPE>
-__global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_symbolic_st(
-    const int32_t *tcol, const RowRef *list, int32_t count, uint32_t S, uint32_t W, uint32_t D,
-    int32_t *nnz_row, Bitmap bm, const int64_t *dup_off, int32_t *dupn, int32_t *gdupt) {
-    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
-    using TM = Team<TEAM>;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    unsigned char *base = smem + (size_t)team * sym_team_bytes(S, W, D);
-    const size_t tab = 2 * round16(4ull * S);
-    int32_t *keys = (int32_t *)base;
-    uint32_t *minp = (uint32_t *)(base + round16(4ull * S));
-    uint32_t *lbits = (uint32_t *)(base + tab);
-    uint32_t *lpref = (uint32_t *)(base + tab + round16(4ull * W));
-    uint2 *dups = (uint2 *)(base + tab + 2 * round16(4ull * W));
-    int *scratch = (int *)(base + tab + 2 * round16(4ull * W) + round16(8ull * D));
-    SymTable<true> tb{keys, minp, S};
-    const int lane = TM::lane();
-    const int64_t nteams = (int64_t)gridDim.x * TPW;
-    int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    RowRef ref = ref_at(list, idx, count);
-    int32_t c[K];
-    load_step<TEAM, K>(tcol, ref, 0, c);
-    while (ref.row >= 0) {
-        Timer tmr;
-        tmr.start();
-        const RowRef next = ref_at(list, idx + nteams, count);
-        uint32_t ndup = 0;
-        const int32_t n = symbolic_row_st<TEAM, K>(tcol, ref, next, c, tb, scratch, lbits, W, dups, D, ndup,
-                                                   tmr);
-        const int64_t row = ref.row;
-        const int64_t off = bm.off[row];
-        // bitmap words and their exclusive prefix popcounts (team-uniform loop)
-        const uint32_t nw = ((uint32_t)ref.n + 31) / 32;
-        int carry = 0;
-        for (uint32_t w0 = 0; w0 < nw; w0 += TEAM) {
-            const uint32_t w = w0 + lane;
-            const uint32_t word = w < nw ? lbits[w] : 0u;
-            int tot;
-            const int ex = TM::excl_sum(__popc(word), tot, scratch);
-            if (w < nw) {
-                bm.bits[off + w] = word;
-                bm.pref[off + w] = (uint32_t)(carry + ex);
-                lpref[w] = (uint32_t)(carry + ex);
-            }
-            carry += tot;
-        }
-        tmr.mark(6);
-        const bool fits = ndup <= D;
-        if (fits && ndup > 0) {
-            TM::sync();   // lpref complete
-            // duplicate i of the list lands at its product-order index d = p - rank(p)
-            for (uint32_t i = lane; i < ndup; i += TEAM) {
-                const uint2 e = dups[i];
-                const uint32_t w = e.x >> 5;
-                const uint32_t rk = lpref[w] + (uint32_t)__popc(lbits[w] & ((1u << (e.x & 31)) - 1u));
-                gdupt[dup_off[row] + (e.x - rk)] = (int32_t)e.y;
-            }
-        }
-        if (lane == 0) {
-            nnz_row[row] = n;
-            dupn[row] = fits ? (int32_t)ndup : -1;
-        }
-        tmr.mark(7);
-        tmr.flush(ilog2(TEAM), lane == 0);
-        TM::sync();   // lbits / dups / scratch are reused by the next row
-        ref = next;
-        idx += nteams;
-    }
 }
 
 // One workgroup per (row, hash partition): distinct columns of the partition
@@ -796,31 +688,6 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const 
                                            bm.pref + bm.off[row], seg, scratch, out, overflow);
 }
 
-// Streaming rows, flat over A entries (numeric_flat_chunk): 4 waves per
-// workgroup, each wave a FLAT_CHUNK-entry chunk at a time (grid-stride).
-constexpr int FLAT_BLOCK = 256;
-#ifndef FLAT_K
-#define FLAT_K 4
-#endif
-#ifndef FLAT_WPE
-#define FLAT_WPE 4
-#endif
-
-__global__ __launch_bounds__(FLAT_BLOCK) __attribute__((amdgpu_waves_per_eu(FLAT_WPE))) void k_numeric_flat(AxView ax, Rows B, FlatArgs fa, Out out) {
-    __shared__ FlatEntry ent[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ unsigned long long masks[FLAT_BLOCK / WAVE][FLAT_MW];
-    const int w = threadIdx.x / WAVE;
-    const int64_t nchunks = (fa.n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
-    const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
-    const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
-    for (int64_t ch = wid; ch < nchunks; ch += nw) {
-        numeric_flat_chunk<FLAT_K>(ax, B, fa, out, ch * FLAT_CHUNK, ent[w], masks[w]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-}
-
 // Duplicate fix-up of the streaming rows that have duplicates: one wave per row.
 constexpr int FIX_TPW = 4;
 __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int32_t count, Bitmap bm,
@@ -884,10 +751,9 @@ __global__ __launch_bounds__(256) void k_fixup_tiny(const RowRef *list, int32_t 
 }
 
 // Duplicate fix-up of streaming rows with long duplicate lists (sort-based).
-#ifndef FIXBIG_CAP_DEF
-#define FIXBIG_CAP_DEF 8192   // 16384 (128 KB of LDS, one block per CU): K3 37.3 vs 36.0 ms
-#endif
-constexpr int FIXBIG_CAP = FIXBIG_CAP_DEF;   // keys (then values) in dynamic LDS: 8 B each, + run-head bits
+// keys (then values) in dynamic LDS: 8 B each, + run-head bits (16384, 128 KB
+// of LDS and one block per CU: K3 37.3 vs 36.0 ms)
+constexpr int FIXBIG_CAP = 8192;
 constexpr size_t FIXBIG_LDS = 8ull * FIXBIG_CAP + FIXBIG_CAP / 8;
 // Lists of at most FIXMID_CAP: 256 lanes and 16 KB of LDS, so several rows per
 // CU (and room beside the streaming pass's waves); longer lists: k_fixup_large
@@ -953,102 +819,6 @@ __global__ void k_row_poff(Rows A, int64_t rows, const int64_t *axp, int64_t n_e
     poff[r] = axp[q];
 }
 
-// Product -> entry mapping without a per-product search: the wave's chunk of
-// entries is compacted to its non-empty entries; for a segment of MW windows
-// of 64 consecutive products, every entry sets the bit of its first product
-// in its window's 64-bit mask (one LDS atomicOr per entry); lane l of a
-// window then belongs to entry ecur + popcount(mask & bits 0..l), and ecur
-// advances by popcount(mask) per window.
-__global__ __launch_bounds__(FLAT_BLOCK) void k_expand(AxView ax, const int64_t *axp, int64_t n_entries,
-                                                       Rows B, int32_t *tcol) {
-    __shared__ int64_t cbs[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ int32_t cpref[FLAT_BLOCK / WAVE][FLAT_CHUNK];
-    __shared__ unsigned long long masks[FLAT_BLOCK / WAVE][FLAT_MW];
-    const int w = threadIdx.x / WAVE;
-    const int lane = threadIdx.x & (WAVE - 1);
-    const uint64_t upto = (2ull << lane) - 1ull;   // bits 0..lane
-    const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
-    const int64_t wid = (int64_t)blockIdx.x * (FLAT_BLOCK / WAVE) + w;
-    const int64_t nw = (int64_t)gridDim.x * (FLAT_BLOCK / WAVE);
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    for (int64_t ch = wid; ch < nchunks; ch += nw) {
-        const int64_t q = ch * FLAT_CHUNK + lane;
-        int len = 0;
-        int64_t g = 0, bsq = 0;
-        if (q < n_entries) {
-            len = ax.blen[q];
-            g = axp[q];
-            bsq = ax.bstart[q];
-        }
-        int x = len;
-#pragma unroll
-        for (int d = 1; d < WAVE; d <<= 1) {
-            const int t = __shfl_up(x, d);
-            if (lane >= d) x += t;
-        }
-        const int T = __shfl(x, WAVE - 1);
-        const int start = x - len;   // chunk-relative first product
-        const int64_t G0 = __shfl(g, 0) ;   // products of the chunk are tcol[G0 .. G0 + T)
-        const uint64_t nz = __ballot(len > 0);
-        if (len > 0) {
-            const int ci = __popcll(nz & ((1ull << lane) - 1ull));
-            cbs[w][ci] = bsq;
-            cpref[w][ci] = start;
-        }
-        for (int seg0 = 0; seg0 < T; seg0 += WAVE * FLAT_MW) {
-            masks[w][lane] = 0ull;   // FLAT_MW == WAVE
-            wave_sync();
-            if (len > 0 && start >= seg0 && start < seg0 + WAVE * FLAT_MW)
-                atomicOr(&masks[w][(start - seg0) >> 6], 1ull << ((start - seg0) & 63));
-            int ecur = __popcll(__ballot(len > 0 && start < seg0)) - 1;
-            wave_sync();
-            const int nwin = min(FLAT_MW, (T - seg0 + WAVE - 1) / WAVE);
-            // loads of window group i+1 go out before the stores of group i (vmcnt order)
-            constexpr int EK = 8;
-            int32_t c[EK], cn[EK];
-            int tt[EK], tn[EK];
-            auto load = [&](int w0, int32_t (&cc)[EK], int (&ti)[EK]) {
-#pragma unroll
-                for (int k = 0; k < EK; ++k) {
-                    ti[k] = -1;
-                    if (w0 + k < nwin) {
-                        const uint64_t m = masks[w][w0 + k];
-                        const int e = ecur + __popcll(m & upto);
-                        ecur += __popcll(m);
-                        const int t = seg0 + (w0 + k) * WAVE + lane;
-                        if (t < T) {
-                            cc[k] = B.col[cbs[w][e] + (t - cpref[w][e])];
-                            ti[k] = t;
-                        }
-                    }
-                }
-            };
-            load(0, c, tt);
-            for (int w0 = 0; w0 < nwin; w0 += EK) {
-                if (w0 + EK < nwin) load(w0 + EK, cn, tn);
-#pragma unroll
-                for (int k = 0; k < EK; ++k)
-                    if (tt[k] >= 0) {
-#if STREAM_NT
-                        __builtin_nontemporal_store(c[k], &tcol[G0 + tt[k]]);
-#else
-                        tcol[G0 + tt[k]] = c[k];
-#endif
-                    }
-#pragma unroll
-                for (int k = 0; k < EK; ++k) {
-                    c[k] = cn[k];
-                    tt[k] = tn[k];
-                }
-            }
-            wave_sync();
-        }
-    }
-}
 
 template <int TEAM, int K, int SEG>
 __global__ __launch_bounds__(TEAM) void k_numeric_global(AxView ax, Rows B, const RowRef *list,
@@ -1365,28 +1135,24 @@ using namespace ias;
 using namespace ias::dev;
 
 // Bin tables.
-//  * Symbolic: rows by products into keys-only LDS tables (load <= 2/3, any
-//    slot count); beyond SYM_MAX products a row is hash-partitioned
-//    (SYM_MAX products per partition) and gets a first-touch bitmap.
+//  * Symbolic: rows by products (SYM2_BINS: short / sym3 / sym2 kernels);
+//    beyond SYM2_MAX products a row is hash-partitioned (SYM_PART_CAP
+//    products per partition) and gets a first-touch bitmap.
 //  * Numeric: rows by nnz.  Rows with many duplicate products (products >
 //    1.5 nnz) and nnz <= VAL_MAX use value tables (16 B/slot, LDS-staged
 //    emission); all others use direct-write tables (8 B/slot) up to DW_MAX;
 //    beyond DW_MAX a row is hash-partitioned (direct write, bitmap ranks);
 //    rows at >= 2^19 - 1 nnz (beyond the 19-bit rank field) use a per-row
-//    table in global memory.  DW_MAX >= SYM_MAX, so every partitioned
-//    numeric row has a bitmap.
+//    table in global memory.  Every row above DW_MAX nnz has more than
+//    SYM2_MAX products, so every partitioned numeric row has a bitmap.
 static inline unsigned grid_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
 
-constexpr int32_t SYM_MAX = 10922;
 constexpr int32_t VAL_MAX = 5460;
 constexpr int32_t DW_MAX = 10922;
-#ifndef SYM_PART_LOG2S
-#define SYM_PART_LOG2S 14   // table slots of a symbolic partition (2^14 = 128 KB of LDS)
-#endif
+constexpr int SYM_PART_LOG2S = 14; // table slots of a symbolic partition (2^14 = 128 KB of LDS)
 constexpr int32_t SYM_PART_CAP = ((1 << SYM_PART_LOG2S) * 2) / 3;   // products per symbolic partition
 constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
-static_assert(DW_MAX >= SYM_MAX, "numeric partitions need the symbolic bitmap");
 
 // LDS bins: upper bound of the key and kernel configuration; table slots
 // S = ceil(1.5 * upper).
@@ -1394,103 +1160,47 @@ struct BinCfg {
     int32_t upper;
     int32_t cfg;
 };
-static constexpr BinCfg SYM_BINS[] = {{64, 0},   {128, 1},  {256, 2},  {512, 3},  {1024, 4},
-                                      {1536, 5}, {2048, 5}, {2730, 5}, {3640, 6}, {4550, 6},
-                                      {5460, 6}, {7280, 7}, {9100, 7}, {SYM_MAX, 7}};
 // value-table config of the <= 16-entry bin: 8-lane teams, 4 products per
 // lane (K1: 101 vs 130 us with 16-lane teams; 32- / 64-lane teams 214 / 254
 // us; 8 products per lane 171 us)
-#ifndef VAL_CFG16
-#define VAL_CFG16 9
-#endif
+constexpr int VAL_CFG16 = 9;
 static constexpr BinCfg VAL_BINS[] = {{16, VAL_CFG16},   {32, 0},   {64, 1},   {128, 2},  {256, 3},
                                       {512, 4},  {768, 5},  {1024, 5}, {1365, 5}, {1820, 6},
                                       {2430, 6}, {3240, 7}, {4320, 7}, {VAL_MAX, 7}};
 static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2},   {256, 3},
                                      {512, 4},  {768, 5},  {1024, 5}, {1536, 6},  {2048, 6},
                                      {3072, 7}, {4096, 7}, {6144, 7}, {8192, 7},  {DW_MAX, 7}};
-constexpr int N_SYM = sizeof(SYM_BINS) / sizeof(SYM_BINS[0]);
-// sym2 (sym2_kernels.hpp, the default): rows up to SYM2_MAX products whose
+// sym2 (sym2_kernels.hpp): rows up to SYM2_MAX products whose
 // entry count fits (8 * entries <= bound) gather from B; the rest are
 // hash-partitioned.  cfg: 0..3 = one-wave teams (K = 1 .. 8 products per
 // lane, 4 teams per workgroup: no workgroup barrier per row), 4..7 = 128- to
 // 1024-lane teams with K = 8 (one-wave teams with K = 16 / 32 measured slower:
 // 160-256 VGPRs, 2-3 waves per SIMD).
-#ifndef SYM2_CFG7_ALT
-#define SYM2_CFG7_ALT 0
-#endif
-#ifndef SYM2_WIDE
-#define SYM2_WIDE 1   // rows of 8193..16384 products on sym2 (else the partitioned path)
-#endif
-constexpr int32_t SYM2_MAX = SYM2_WIDE ? 16384 : 8192;
+constexpr int32_t SYM2_MAX = 16384;
 constexpr int SYM2_WAVE_CFG_MAX = 3;
 constexpr int SYM2_CFG_WIDE = 8;   // 16 products per lane of a 1024-lane team, one-wave (compact) layout
 static constexpr BinCfg SYM2_BINS[] = {{64, 0},    {128, 1},  {256, 2},  {512, 3},  {768, 4},
                                        {1024, 4},  {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6},
                                        {6144, 7},  {8192, 7},
-#if SYM2_WIDE
                                        {12288, SYM2_CFG_WIDE}, {SYM2_MAX, SYM2_CFG_WIDE}
-#endif
 };
 constexpr int N_SYM2 = sizeof(SYM2_BINS) / sizeof(SYM2_BINS[0]);
-static bool sym2_on() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_SYM2");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-// IAS_NUM2=0: the streaming rows take the flat numeric pass (k_numeric_flat)
-// instead of the row-unit pass with LDS-staged C writes (k_num2).
-static bool num2_on() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_NUM2");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-// IAS_N2_SPLIT=0: one k_num2 launch, the fix-ups after it on its stream
-// (default: up to three launches — units of rows with > 1024 duplicates, with
-// fewer, without — the longest lists' 1024-lane fix-ups right after the first
-// launch on its stream, the other fix-ups of each class on another stream
-// alongside the later launches).
-static bool n2_split_on() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_N2_SPLIT");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
 static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
-static_assert(N_SYM + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
+static_assert(N_SYM2 + 3 <= MAX_BINS && N_VAL + N_DW + 6 <= MAX_BINS, "bins");
 
 // table slots of an LDS bin: 1.5 x its bound, a whole number of 4-slot buckets
-#ifndef SLOT_NUM
-#define SLOT_NUM 3   // slots per bound: SLOT_NUM / 2
-#endif
+constexpr int SLOT_NUM = 3; // slots per bound: SLOT_NUM / 2
 static constexpr uint32_t slots_for(int32_t upper) {
     return (uint32_t)(((SLOT_NUM * (long long)upper + 1) / 2 + 3) / 4 * 4);
 }
-// symbolic LDS bins may use a lower load where LDS is not the limit
-#ifndef SYM_SLOT_NUM_SMALL
-#define SYM_SLOT_NUM_SMALL 3
-#endif
-static constexpr uint32_t sym_slots_for(int32_t upper) {
-    return upper <= 1024 ? (uint32_t)(((SYM_SLOT_NUM_SMALL * (long long)upper + 1) / 2 + 3) / 4 * 4)
-                         : slots_for(upper);
-}
-// first-touch words staged per row: whole 64-bit ballots (2 words per 64 products)
-static constexpr uint32_t words_for(int32_t upper) { return (uint32_t)(2 * ((upper + 63) / 64)); }
 // duplicate-list capacity of a symbolic bin: rows with more duplicate
 // products than this take the table path in the numeric pass
 static constexpr int32_t dcap_for(int32_t upper) {
     return upper / 8 < 8 ? 8 : (upper / 8 > 2048 ? 2048 : upper / 8);
 }
-#ifndef PART_DCAP_DIV
-#define PART_DCAP_DIV 4   // partitioned rows: list of min(products / PART_DCAP_DIV, FIXBIG_CAP); 8: K3 38.96 vs 36.27 ms
-#endif
+constexpr int PART_DCAP_DIV = 4; // partitioned rows: list of min(products / PART_DCAP_DIV, FIXBIG_CAP); 8: K3 38.96 vs 36.27 ms
 
 // TEAM * PER of each value configuration in val_bin(): the emission loop
 // visits that many slots, so it must cover every bin's S.
@@ -1505,20 +1215,12 @@ static_assert(val_bins_covered(), "value-bin emission does not cover a bin's tab
 static BinSpec sym_spec() {
     BinSpec s{};
     s.ndw = 0;
-    if (sym2_on()) {
-        s.nval = N_SYM2;
-        for (int i = 0; i < N_SYM2; ++i) {
-            s.upper[i + 1] = SYM2_BINS[i].upper;
-            s.dcap[i + 1] = dcap_for(SYM2_BINS[i].upper);
-        }
-        s.ent_key = 8;   // the row's non-empty entries are staged in LDS, upper/8 of them
-    } else {
-        s.nval = N_SYM;
-        for (int i = 0; i < N_SYM; ++i) {
-            s.upper[i + 1] = SYM_BINS[i].upper;
-            s.dcap[i + 1] = dcap_for(SYM_BINS[i].upper);
-        }
+    s.nval = N_SYM2;
+    for (int i = 0; i < N_SYM2; ++i) {
+        s.upper[i + 1] = SYM2_BINS[i].upper;
+        s.dcap[i + 1] = dcap_for(SYM2_BINS[i].upper);
     }
+    s.ent_key = 8;   // the row's non-empty entries are staged in LDS, upper/8 of them
     s.ratio_num = 0;
     s.ratio_den = 0;
     s.part_cap = SYM_PART_CAP;
@@ -1550,18 +1252,8 @@ static BinSpec num_spec() {
 static_assert(N_VAL + 3 + N_DW + 3 + 3 <= MAX_BINS, "short bins beyond MAX_BINS");
 
 // Rows of at most SHORT_MAX products take the short path (short_kernels.hpp:
-// one wave per row, exact LDS table, no bitmap) in both passes; IAS_SHORT=0
-// sends them through sym2 + the streaming numeric pass instead.
-#ifndef SHORT_MAX
-#define SHORT_MAX 256
-#endif
-static bool short_on() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_SHORT");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
+// one wave per row, exact LDS table, no bitmap) in both passes.
+constexpr int32_t SHORT_MAX = 256;
 
 // Dynamic LDS beyond 64 KiB is requested per kernel (once per instantiation:
 // the callers below are templates, so each has its own flag).
@@ -1611,64 +1303,22 @@ static int64_t resident_blocks(F kernel, int threads, size_t lds) {
 // One wave per row (the kernels' grid-stride loop then runs once): measured
 // faster than persistent waves capped at the resident count with the next
 // row prefetched (K2: 0.99 / 1.46 ms vs 1.16 / 1.56 ms symbolic / numeric).
-// IAS_SHORT_PERSIST=1 caps the grid at the resident workgroups instead.
-template <typename F>
-static unsigned short_grid(F kern, int32_t count) {
-    static const bool persist = [] {
-        const char *e = getenv("IAS_SHORT_PERSIST");
-        return e && *e == '1';
-    }();
-    const int64_t want = (count + SH_WPB - 1) / SH_WPB;
-    if (!persist) return (unsigned)std::max<int64_t>(1, want);
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, resident_blocks(kern, 64 * SH_WPB, 0)));
+static unsigned short_grid(int32_t count, int rows_per_wave = 1) {
+    const int64_t per = (int64_t)SH_WPB * rows_per_wave;
+    return (unsigned)std::max<int64_t>(1, ((int64_t)count + per - 1) / per);
 }
-// SH_SYM_R rows per wave in the short symbolic pass for rows of <= 128
-// products (1: the one-row kernel below); rows of 129..256 products one per
-// wave with the 4-slots-per-product table (SH_SYM_R4 = 2: two per wave)
-#ifndef SH_SYM_R
-#define SH_SYM_R 2
-#endif
-#ifndef SH_SYM_R4
-#define SH_SYM_R4 1
-#endif
-static unsigned short_grid_r(int32_t count, int r) {
-    return (unsigned)std::max<int64_t>(1, ((int64_t)count + SH_WPB * r - 1) / (SH_WPB * r));
-}
+// The short symbolic pass: two rows per wave for rows of <= 128 products; rows
+// of 129..256 products one per wave with the 4-slots-per-product table.
 static void short_sym_launch(int32_t upper, const ShortArgs &a, hipStream_t t) {
-    if (SH_SYM_R > 1) {
-        constexpr int R = SH_SYM_R > 1 ? SH_SYM_R : 2;
-        const unsigned g = short_grid_r(a.count, R);
-        if (upper <= 64) k_short_sym_r<1, R><<<g, 64 * SH_WPB, 0, t>>>(a);
-        else if (upper <= 128) k_short_sym_r<2, R><<<g, 64 * SH_WPB, 0, t>>>(a);
-        else if (SH_SYM_R4 > 1) k_short_sym_r<4, R><<<g, 64 * SH_WPB, 0, t>>>(a);
-        else k_short_sym<4><<<short_grid(k_short_sym<4>, a.count), 64 * SH_WPB, 0, t>>>(a);
-        return;
-    }
-    if (upper <= 64) k_short_sym<1><<<short_grid(k_short_sym<1>, a.count), 64 * SH_WPB, 0, t>>>(a);
-    else if (upper <= 128) k_short_sym<2><<<short_grid(k_short_sym<2>, a.count), 64 * SH_WPB, 0, t>>>(a);
-    else k_short_sym<4><<<short_grid(k_short_sym<4>, a.count), 64 * SH_WPB, 0, t>>>(a);
+    constexpr int R = 2;
+    if (upper <= 64) k_short_sym_r<1, R><<<short_grid(a.count, R), 64 * SH_WPB, 0, t>>>(a);
+    else if (upper <= 128) k_short_sym_r<2, R><<<short_grid(a.count, R), 64 * SH_WPB, 0, t>>>(a);
+    else k_short_sym<4><<<short_grid(a.count), 64 * SH_WPB, 0, t>>>(a);
 }
 static void short_num_launch(int i, const ShortArgs &a, const Out &out, hipStream_t t) {
-    if (i == 0) k_short_num<1><<<short_grid(k_short_num<1>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
-    else if (i == 1) k_short_num<2><<<short_grid(k_short_num<2>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
-    else k_short_num<4><<<short_grid(k_short_num<4>, a.count), 64 * SH_WPB, 0, t>>>(a, out);
-}
-
-// IAS_PART_BUCKET=0: partitioned rows rescan their expansion per partition
-// instead of bucketing it once (k_part_bucket).
-static bool part_bucket() {
-    const char *e = getenv("IAS_PART_BUCKET");
-    return !(e && *e == '0');
-}
-
-// IAS_SYM_PERSIST=1: symbolic teams persist over their bin (grid = resident
-// workgroups) instead of one team per row.
-static bool sym_persist() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_SYM_PERSIST");
-        return e && *e && *e != '0';
-    }();
-    return on;
+    if (i == 0) k_short_num<1><<<short_grid(a.count), 64 * SH_WPB, 0, t>>>(a, out);
+    else if (i == 1) k_short_num<2><<<short_grid(a.count), 64 * SH_WPB, 0, t>>>(a, out);
+    else k_short_num<4><<<short_grid(a.count), 64 * SH_WPB, 0, t>>>(a, out);
 }
 
 struct Launch {
@@ -1688,50 +1338,8 @@ struct StArgs {
     int32_t *dupt;
 };
 
-template <int TEAM, int K, int TPW, int WPE>
-static void sym_launch(const Launch &l, const int32_t *tcol, uint32_t W, uint32_t D, int32_t *nnz,
-                       const StArgs &a) {
-    auto kern = k_symbolic_st<TEAM, K, TPW, WPE>;
-    static bool done = false;
-    const size_t lds = (size_t)TPW * sym_team_bytes(l.S, W, D);
-    allow_lds(kern, done, lds);
-    int64_t grid = grid_for(l.c, TPW);
-    if (sym_persist()) grid = std::min<int64_t>(grid, resident_blocks(kern, TEAM * TPW, lds));
-    kern<<<(unsigned)grid, TEAM * TPW, lds, l.s>>>(tcol, l.list, l.c, l.S, W, D, nnz, a.bm, a.dup_off,
-                                                   a.dupn, a.dupt);
-}
-
-// items per lane of the multi-wave symbolic teams (a step of TEAM * K
-// products ends in a workgroup barrier)
-#ifndef SYM_K5
-#define SYM_K5 4
-#endif
-#ifndef SYM_K6
-#define SYM_K6 4
-#endif
-#ifndef SYM_K7
-#define SYM_K7 2
-#endif
-#ifndef SYM_WPE_SMALL
-#define SYM_WPE_SMALL 7   // waves per SIMD the register budget of the wave-level teams allows
-#endif
-static void sym_bin(int cfg, const Launch &l, const int32_t *tcol, uint32_t W, uint32_t D, int32_t *nnz,
-                    const StArgs &a) {
-    switch (cfg) {
-        case 0: sym_launch<16, 4, 16, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
-        case 1: sym_launch<32, 4, 8, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
-        case 2: sym_launch<64, 4, 4, SYM_WPE_SMALL>(l, tcol, W, D, nnz, a); break;
-        case 3: sym_launch<64, 8, 4, 4>(l, tcol, W, D, nnz, a); break;
-        case 4: sym_launch<128, 4, 1, 6>(l, tcol, W, D, nnz, a); break;
-        case 5: sym_launch<256, SYM_K5, 1, 1>(l, tcol, W, D, nnz, a); break;
-        case 6: sym_launch<512, SYM_K6, 1, 1>(l, tcol, W, D, nnz, a); break;
-        default: sym_launch<1024, SYM_K7, 1, 1>(l, tcol, W, D, nnz, a); break;
-    }
-}
-
 static Sym2Layout sym2_layout(int32_t upper, int cfg) {
     // 8 filter bits keep the widest bin's team within one CU's LDS
-    if (SYM2_CFG7_ALT && cfg == 7) return Sym2Layout::for_bound((uint32_t)upper, Sym2Layout::ONE_WAVE);
     return Sym2Layout::for_bound((uint32_t)upper, cfg == SYM2_CFG_WIDE     ? Sym2Layout::WIDE
                                                   : cfg <= SYM2_WAVE_CFG_MAX ? Sym2Layout::ONE_WAVE
                                                                              : Sym2Layout::TEAM_LAYOUT);
@@ -1748,9 +1356,7 @@ static void sym2_launch(Sym2Args a, hipStream_t s) {
     kern<<<(unsigned)std::max<int64_t>(grid, 1), TEAM * TPW, lds, s>>>(a);
 }
 
-#ifndef SYM2_WPE_TEAM
-#define SYM2_WPE_TEAM 1   // waves per SIMD the multi-wave teams' registers must allow (1: no cap)
-#endif
+constexpr int SYM2_WPE_TEAM = 1; // waves per SIMD the multi-wave teams' registers must allow (1: no cap)
 static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
     switch (cfg) {
         case 0: sym2_launch<64, 1, 4>(a, s); break;
@@ -1760,34 +1366,16 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
         case 4: sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(a, s); break;   // one-wave K=16 measured 30 % slower
         case 5: sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(a, s); break;
         case 6: sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(a, s); break;
-#if SYM2_CFG7_ALT
-        case 7: sym2_launch<512, 16, 1, 4>(a, s); break;   // A/B: two teams per CU, compact layout
-#else
         case 7: sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(a, s); break;
-#endif
         default: sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(a, s); break;   // SYM2_CFG_WIDE
     }
 }
 
-// IAS_SYM3=0: the 257 .. 1024-product rows take sym2's teams instead of
-// sym3's one-wave rows (sym3_kernels.hpp).
-static bool sym3_on() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_SYM3");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-#ifndef SYM3_MAX_DEF
-#define SYM3_MAX_DEF 2048
-#endif
-constexpr int32_t SYM3_MIN = 257, SYM3_MAX = SYM3_MAX_DEF;
-#ifndef SYM3_WPB
-#define SYM3_WPB 4
-#endif
-#ifndef SYM3_DB_MAXK
-#define SYM3_DB_MAXK 8   // K up to which the next row's columns are gathered during a row (registers)
-#endif
+
+// sym3's one-wave rows (sym3_kernels.hpp): rows of SYM3_MIN .. SYM3_MAX products
+constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 2048;
+constexpr int SYM3_WPB = 4;
+constexpr int SYM3_DB_MAXK = 8; // K up to which the next row's columns are gathered during a row (registers)
 template <int K>
 static void sym3_launch(const Sym3Args &a, hipStream_t s) {
     auto kern = k_sym3<K, SYM3_WPB, (K <= SYM3_DB_MAXK)>;
@@ -1909,10 +1497,6 @@ ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
 
 ias_plan::~ias_plan() {
     hipSetDevice(device);
-    for (auto &q : pipe) {
-        delete q;
-        q = nullptr;
-    }
     if (stream) hipStreamSynchronize((hipStream_t)stream);
     for (auto &b : bufs)
         if (b.p) hipFree(b.p);
@@ -1990,8 +1574,7 @@ AxView ias_plan::ax_view() {
 
 // Analysis (queued, no host wait): products per row, expanded A, product
 // offsets per entry and per row, symbolic bin counts into the B_CNT counters.
-ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries,
-                                     bool need_rows) {
+ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries) {
     hipStream_t s = (hipStream_t)stream;
     HIPC(hipSetDevice(device));
     n_rows = rows;
@@ -2000,7 +1583,6 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
-    IAS_TRY(reserve(B_AXR, sizeof(int32_t) * ae));
     IAS_TRY(reserve(B_AXP, sizeof(int64_t) * (ae + 1)));
     IAS_TRY(reserve(B_POFF, sizeof(int64_t) * (rows + 1)));
     const int64_t nbe = (a_entries + SCAN_TILE - 1) / SCAN_TILE;
@@ -2018,24 +1600,18 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
     IAS_TRY(reserve(B_PART, sizeof(int64_t) * (3 * nb + 4)));   // also the 3*rows scan of the num2 units
     Counters *dc = as<Counters>(bufs[B_CNT]);
-    Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
 
     // ---- analysis: products per row, expanded A (+ product offsets), symbolic bin counts
     HIPC(hipEventRecord(ev[0], s));
     HIPC(hipMemsetAsync(dc, 0, 2 * sizeof(Counters), s));   // dc, dc2
     int32_t *axl = as<int32_t>(bufs[B_AXL]);
-    int32_t *axr = as<int32_t>(bufs[B_AXR]);
     int64_t *axp = as<int64_t>(bufs[B_AXP]);
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
-    // the row of every A entry: only the flat numeric pass (IAS_NUM2=0) and the
-    // single-pass engine read it (k_row_poff validates the row pointer)
-    if (A.ptr && rows > 0 && need_rows)
-        k_an_rowfill<<<grid_for(rows * AN_FILL, 256), 256, 0, s>>>(A, rows, a_entries, axr, dc);
     if (a_entries > 0) {
         const int64_t per = (int64_t)AN_BLOCK * AN_U;
         const unsigned g = (unsigned)std::min<int64_t>((a_entries + per - 1) / per, 16384);
         k_an_entries<<<g, AN_BLOCK, 0, s>>>(A, B, a_entries,
-                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, axr, &dc->wide_b});
+                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, &dc->wide_b});
     }
     CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
@@ -2056,7 +1632,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
 ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
                               int64_t a_entries, ias_report *rep) {
     (void)cols;
-    IAS_TRY(analysis_launch(A, B, rows, a_entries, !num2_on()));
+    IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
     const BinSpec ss = sym_spec(), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
@@ -2078,25 +1654,18 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     small = flops < SMALL_FLOPS;
     max_prod = c1.max_prod;
 
-    // ---- expansion: every row's product columns, contiguous (sym2: only the
-    // partitioned rows', in their compact space; the LDS bins gather from B)
-    const bool sym2 = sym2_on();
-    IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>(sym2 ? (int64_t)c1.part_prod : flops, 1)));
+    // ---- expansion of the partitioned rows' product columns (in their
+    // compact space; the other bins gather from B)
+    IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>((int64_t)c1.part_prod, 1)));
     const int32_t *tcol = as<int32_t>(bufs[B_TCOL]);
-    if (a_entries > 0 && !sym2) {
-        const int64_t nchunks = (a_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
-        const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 4096);
-        k_expand<<<grid, FLAT_BLOCK, 0, s>>>(ax, axp, a_entries, B, as<int32_t>(bufs[B_TCOL]));
-    }
-    CHECK_LAUNCH("k_expand", s);
 
     // ---- symbolic binning + symbolic
     IAS_TRY(reserve(B_SITEM, sizeof(PartItem) * (size_t)(c1.items + 1)));
     IAS_TRY(reserve(B_PFIRST, sizeof(int64_t) * (size_t)(rows + 1)));
     IAS_TRY(reserve(B_PBOFF, sizeof(int64_t) * (size_t)(rows + 1)));
     IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
-    if (part_bucket()) IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
-    if (sym3_on() && !c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
+    IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
+    if (!c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -2113,7 +1682,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         BIN_LAUNCH(k_bin_scatter, rows, s, 
             as<int32_t>(bufs[B_PROD]), nullptr, nullptr, rows, ss, A, SL, as<PartItem>(bufs[B_SITEM]),
             as<int64_t>(bufs[B_BMOFF]), nullptr, sa.dup_off, sa.dupn, nnz, poff, dc, as<int64_t>(bufs[B_PFIRST]),
-            as<int64_t>(bufs[B_PBOFF]), sym2 ? 1 : 0);
+            as<int64_t>(bufs[B_PBOFF]), 1);
     CHECK_LAUNCH("k_bin_scatter(symbolic)", s);
     HIPC(hipEventRecord(ev[1], s));
     int64_t st[MAX_BINS];
@@ -2123,40 +1692,32 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int lane_no = 0;
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        const bool pb = part_bucket();
-        if (sym2)
-            k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+        k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                as<int32_t>(bufs[B_TCOL]));
-        if (pb)
-            k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
+        k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
                                                  as<PartSpan>(bufs[B_PSPAN]));
         k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, pb ? as<uint2>(bufs[B_PBKT]) : nullptr,
-            pb ? as<PartSpan>(bufs[B_PSPAN]) : nullptr);
+            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]));
         k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
         k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
                                       sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
-    for (int b = ss.nval; b >= 1 && sym2; --b)
+    for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(lane_no++);
             const int32_t u = SYM2_BINS[b - 1].upper;
-            static const int abl = [] {
-                const char *e = getenv("IAS_S2_ABLATE");
-                return e ? atoi(e) : 0;
-            }();
-            if (u <= SHORT_MAX && short_on()) {
+            if (u <= SHORT_MAX) {
                 const ShortArgs sh{A, ax, B.col, B.val, SL + st[b], c, nnz, sa.dupn};
                 short_sym_launch(u, sh, t);
                 CHECK_LAUNCH("k_short_sym", t);
                 continue;
             }
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
-                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), abl, DW_MAX, nullptr};
-            if (sym3_on() && !c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
+                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
+            if (!c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
                 const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                                   &dc->s3_retry[b & 7]};   // a counter per bin (bins run concurrently)
@@ -2168,14 +1729,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             }
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);
-        }
-    for (int b = ss.nval; b >= 1 && !sym2; --b)
-        if ((c = c1.count[b]) > 0) {
-            hipStream_t t = (hipStream_t)side_stream(lane_no++);
-            const int32_t u = SYM_BINS[b - 1].upper;
-            sym_bin(SYM_BINS[b - 1].cfg, Launch{c, sym_slots_for(u), t, ax, B, SL + st[b]}, tcol, words_for(u),
-                    (uint32_t)dcap_for(u), nnz, sa);
-            CHECK_LAUNCH("k_symbolic_st", t);
         }
     HIPC(hipGetLastError());
     IAS_TRY(join());
@@ -2201,10 +1754,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         // short, as K1 / K2: no unit lists to build)
         bool any_stream = c1.count[sym_part] > 0;
         for (int b = 1; b <= ss.nval; ++b) {
-            const int32_t u = sym2 ? SYM2_BINS[b - 1].upper : SYM_BINS[b - 1].upper;
-            if (c1.count[b] > 0 && !(sym2 && u <= SHORT_MAX && short_on())) any_stream = true;
+            if (c1.count[b] > 0 && SYM2_BINS[b - 1].upper > SHORT_MAX) any_stream = true;
         }
-        if (num2_on() && any_stream) {
+        if (any_stream) {
             // work units of the row-unit numeric pass: 64 A entries of a streaming row
             // (ordered by class: rows with > 256 duplicates, with fewer,
             // without — each class's fix-ups can start once its units are done)
@@ -2309,11 +1861,6 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     if (n_entries > 0) {
         if (!serial && !small && lane_no < 2) lane_no = 2;
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        const FlatArgs fa{as<int32_t>(bufs[B_AXR]), as<int64_t>(bufs[B_AXP]), as<int64_t>(bufs[B_POFF]),
-                          n_entries, as<int32_t>(bufs[B_TCOL]), bm, sa.dupn, sa.dup_off,
-                          as<double>(bufs[B_DUPV])};
-        const int64_t nchunks = (n_entries + FLAT_CHUNK - 1) / FLAT_CHUNK;
-        const unsigned grid = (unsigned)std::min<int64_t>(grid_for(nchunks, FLAT_BLOCK / WAVE), 2048);
         // fix-ups of the rows with duplicates: on the pass's stream after it,
         // or (split) the 1024-lane sorted fix-ups (> 4096 duplicates) on the
         // pass's stream right after their rows' units (they need whole CUs:
@@ -2358,11 +1905,11 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
             return IAS_SUCCESS;
         };
         HIPC(hipEventRecord(ev[5], t));
-        if (num2_on()) {
+        {
             if (n2_units > 0) {
-                Num2Args na{A, ax, fa.axp, fa.poff, B.col, B.val, as<Num2Unit>(bufs[B_N2UNIT]), n2_units,
-                            bm, sa.dup_off, fa.dupval};
-                fix_split = fixups && !serial && !small && n2_split_on();
+                Num2Args na{A, ax, as<int64_t>(bufs[B_AXP]), as<int64_t>(bufs[B_POFF]), B.col, B.val,
+                            as<Num2Unit>(bufs[B_N2UNIT]), n2_units, bm, sa.dup_off, as<double>(bufs[B_DUPV])};
+                fix_split = fixups && !serial && !small;
                 // units by class: [0, bunits) rows with > 1024 duplicates,
                 // [bunits, dunits) with fewer, [dunits, units) without
                 const int64_t cut[4] = {0, fix_split ? n2_bunits : 0, fix_split ? n2_dunits : 0, n2_units};
@@ -2383,11 +1930,9 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                 }
                 fix_lane = lane_no;   // the fix-ups: the stream after this one
             }
-        } else {
-            k_numeric_flat<<<grid, FLAT_BLOCK, 0, t>>>(ax, B, fa, out);
         }
         HIPC(hipEventRecord(ev[6], t));
-        CHECK_LAUNCH("k_numeric_flat", t);
+        CHECK_LAUNCH("k_num2", t);
         if (!fix_split) IAS_TRY(launch_fix(t, 3));
     }
     // short rows: all on the fix-up stream when the pass is split (ahead of
@@ -2419,7 +1964,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         k_fill_rows<<<grid_for(rows * WAVE, 256), 256, 0, s>>>(out.ptr, rows, out.row_idx);
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[4], s));
-    if (num_count[part_bin] > 0 && !defer_checks) {
+    if (num_count[part_bin] > 0) {
         int32_t of = 0;
         HIPC(hipMemcpyAsync(&of, &dc2->overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         HIPC(hipStreamSynchronize(s));
@@ -2455,175 +2000,6 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     return IAS_SUCCESS;
 }
 
-
-// =================================================================== row-block pipeline
-namespace ias {
-namespace dev {
-// Products of every row (sum of its entries' B-row lengths, capped at
-// INT32_MAX): one wave per row, the lanes striding its entries.
-__global__ void k_row_cost(Rows A, Rows B, int64_t rows, int32_t *cost) {
-    const int lane = (int)(threadIdx.x & (WAVE - 1));
-    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-    const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
-    for (int64_t r = w0; r < rows; r += nw) {
-        const int64_t e0 = A.ptr[r], e1 = A.ptr[r + 1];
-        int64_t t = 0;
-        for (int64_t e = e0 + lane; e < e1; e += WAVE) {
-            int64_t bs;
-            int32_t bn;
-            B.row(A.col[e], bs, bn);
-            t += bn;
-        }
-        for (int o = WAVE / 2; o > 0; o >>= 1) t += __shfl_xor(t, o);
-        if (lane == 0) cost[r] = (int32_t)(t < 0x7FFFFFFF ? t : 0x7FFFFFFF);
-    }
-}
-// Block bounds by cost: bounds[b] = the first row whose cost prefix is >=
-// b/NB of the total (binary search over the prefix), plus each bound's A
-// entry offset.
-__global__ void k_row_blocks(const int64_t *ptr, const int64_t *pre, int64_t rows, int32_t nb, int64_t *bounds,
-                             int64_t *ents) {
-    const int b = (int)threadIdx.x;
-    if (b > nb) return;
-    const int64_t tot = pre[rows];
-    int64_t r;
-    if (b == 0) r = 0;
-    else if (b == nb) r = rows;
-    else {
-        const int64_t want = tot * b / nb;
-        int64_t lo = 0, hi = rows;   // first row r with pre[r] >= want
-        while (lo < hi) {
-            const int64_t mid = (lo + hi) / 2;
-            if (pre[mid] < want) lo = mid + 1;
-            else hi = mid;
-        }
-        r = lo;
-    }
-    bounds[b] = r;
-    ents[b] = ptr[r] - ptr[0];
-}
-// C's row pointer of a block: the block's own (from 0) shifted to its place
-__global__ void k_place_ptr(const int64_t *src, int64_t n, int64_t base, int64_t *dst) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = src[i] + base;
-}
-}  // namespace dev
-}  // namespace ias
-
-ias_status ias_plan::pipelined(const Rows &A, const Rows &B, int64_t rows, int64_t cols, int64_t a_entries,
-                               int64_t *c_ptr, int32_t *c_col, double *c_val, int64_t cap, int32_t nb,
-                               int64_t *nnz_c, ias_report *rep) {
-    hipStream_t s = (hipStream_t)stream;
-    HIPC(hipSetDevice(device));
-    if (rows <= 0) {
-        HIPC(hipMemsetAsync(c_ptr, 0, sizeof(int64_t), s));
-        HIPC(hipStreamSynchronize(s));
-        *nnz_c = 0;
-        return IAS_SUCCESS;
-    }
-    nb = (int32_t)std::max<int64_t>(1, std::min<int64_t>({(int64_t)nb, rows, 64}));
-    for (auto &q : pipe)
-        if (!q) {
-            q = new ias_plan();
-            const ias_status st = q->init(device, nullptr);
-            if (st != IAS_SUCCESS) {
-                delete q;
-                q = nullptr;
-                return st;
-            }
-            q->defer_checks = true;  // no host wait inside numeric(): checked at the end
-        }
-    {
-        // IAS_PIPE_SERIAL=1: one stream per sub-plan (no side streams inside a block)
-        const char *e = getenv("IAS_PIPE_SERIAL");
-        const bool ser = e && *e == '1';
-        for (auto q : pipe) q->serial = ser;
-    }
-    HIPC(hipEventRecord(ev[0], s));
-    for (auto q : pipe) HIPC(hipStreamWaitEvent((hipStream_t)q->stream, ev[0], 0));   // after the caller's work
-    // blocks of equal products (R-MAT's low rows hold most of them: blocks of
-    // equal A entries were measured 1.2 ms slower per K3' step than one block)
-    IAS_TRY(reserve(B_TMP0, sizeof(int64_t) * 2 * (size_t)(nb + 1)));
-    IAS_TRY(reserve(B_TMP1, sizeof(int32_t) * (size_t)(rows + 1)));
-    IAS_TRY(reserve(B_TMP2, sizeof(int64_t) * (size_t)(rows + 1)));
-    IAS_TRY(reserve(B_PART, sizeof(int64_t) * (size_t)((rows + SCAN_TILE - 1) / SCAN_TILE + 4)));
-    int64_t *bnd = as<int64_t>(bufs[B_TMP0]), *pre = as<int64_t>(bufs[B_TMP2]);
-    dev::k_row_cost<<<(unsigned)std::min<int64_t>(grid_for(rows * WAVE, 256), 8192), 256, 0, s>>>(
-        A, B, rows, as<int32_t>(bufs[B_TMP1]));
-    scan_i32(as<int32_t>(bufs[B_TMP1]), rows, as<int64_t>(bufs[B_PART]), pre, s);
-    dev::k_row_blocks<<<1, 128, 0, s>>>(A.ptr, pre, rows, nb, bnd, bnd + nb + 1);
-    std::vector<int64_t> hb(2 * (size_t)(nb + 1));
-    HIPC(hipMemcpyAsync(hb.data(), bnd, sizeof(int64_t) * hb.size(), hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
-    const int64_t *rb = hb.data(), *eb = hb.data() + nb + 1;
-    int64_t base = 0, fl = 0, mp = 0, mn = 0;
-    bool over = false;
-    hipEvent_t done[2] = {nullptr, nullptr};
-    for (int b = 0; b < nb; ++b) {
-        const int64_t r0 = rb[b], r1 = rb[b + 1];
-        if (r1 <= r0) continue;
-        ias_plan *P = pipe[b & 1];
-        Rows Ab = A;
-        Ab.ptr = A.ptr + r0;   // a row view: entries addressed absolutely
-        IAS_TRY(P->symbolic(Ab, B, r1 - r0, cols, eb[b + 1] - eb[b], nullptr));
-        fl += P->flops;
-        mp = std::max<int64_t>(mp, P->max_prod);
-        mn = std::max<int64_t>(mn, P->max_nnz);
-        const int64_t nb_nnz = P->nnz_total;
-        hipStream_t t = (hipStream_t)P->stream;
-        if (base + nb_nnz > cap) over = true;
-        // the row pointer is written in full even past the capacity (ias.h)
-        dev::k_place_ptr<<<grid_for(r1 - r0 + 1, 256), 256, 0, t>>>(as<int64_t>(P->bufs[B_PTR]), r1 - r0 + 1,
-                                                                  base, c_ptr + r0);
-        done[b & 1] = P->ev[7];
-        HIPC(hipEventRecord(P->ev[7], t));
-        if (!over) {
-            const Out out{c_ptr + r0, 0, c_col, c_val, nullptr, 0, 0, nullptr};
-            IAS_TRY(P->numeric(Ab, B, out, nullptr));
-            HIPC(hipEventRecord(P->ev[7], t));
-        }
-        base += nb_nnz;
-    }
-    // the plan stream (the caller's) waits for both sub-plans
-    for (auto e : done)
-        if (e) HIPC(hipStreamWaitEvent(s, e, 0));
-    // the partitioned numeric pass's table overflow (deferred in the sub-plans)
-    for (auto q : pipe) {
-        int32_t of = 0;
-        HIPC(hipMemcpyAsync(&of, &(as<Counters>(q->bufs[B_CNT]) + 1)->overflow, sizeof(int32_t),
-                            hipMemcpyDeviceToHost, (hipStream_t)q->stream));
-        HIPC(hipStreamSynchronize((hipStream_t)q->stream));
-        if (of) {
-            set_last_error("hash partition table overflow in the numeric pass");
-            return IAS_ERROR_OVERFLOW;
-        }
-    }
-    if (over) {
-        // row pointer only: C's entries need more than its capacity
-        HIPC(hipStreamSynchronize(s));
-        *nnz_c = base;
-        set_last_error("C needs %lld entries, capacity %lld", (long long)base, (long long)cap);
-        return IAS_ERROR_INSUFFICIENT_CAPACITY;
-    }
-    HIPC(hipEventRecord(ev[4], s));
-    *nnz_c = base;
-    nnz_total = base;
-    flops = fl;
-    max_prod = (int32_t)mp;
-    max_nnz = (int32_t)mn;
-    n_rows = rows;
-    if (rep) {
-        HIPC(hipEventSynchronize(ev[4]));
-        float t = 0;
-        hipEventElapsedTime(&t, ev[0], ev[4]);
-        rep->ms_total = t;
-        rep->flops = fl;
-        rep->nnz_c = base;
-        rep->max_row_products = mp;
-        rep->max_row_nnz = mn;
-    }
-    return IAS_SUCCESS;
-}
 
 // =================================================================== scan
 // Exclusive scan of n int32 values into out[0..n] (out[n] = total), on `s`.

@@ -60,7 +60,7 @@ struct Counters {
 
 struct ias_plan {
     enum {
-        B_AXS, B_AXL, B_AXV, B_AXR, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
+        B_AXS, B_AXL, B_AXV, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
         B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5,
         // partition buckets of the symbolic pass
@@ -89,7 +89,6 @@ struct ias_plan {
     ias_status fork();
     ias_status join();
     bool serial = false;   // IAS_SERIAL=1: everything on `stream` (per-kernel profiling)
-    bool defer_checks = false;   // numeric(): no host wait for the overflow flag (pipeline sub-plans)
     // small products (flops < SMALL_FLOPS): the bins run on `stream` too — a
     // fork / join across queues costs ~30 us of event latency each, more than
     // the bins of a small product overlap
@@ -123,20 +122,11 @@ struct ias_plan {
     ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
     // a_entries: stored entries of A (CSR: nnz of the view; ELL: rows * width)
     ias_status analysis_launch(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
-                               int64_t a_entries, bool need_rows);
+                               int64_t a_entries);
     const double *ax_aval = nullptr;   // A.val + the view's base (set after the analysis read-back)
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                         int64_t cols, int64_t a_entries, ias_report *rep);
     ias::dev::AxView ax_view();
-    // Row-block pipeline (ias_csr_mul_csr_into, one call): A's rows in blocks,
-    // each block's symbolic pass on one of two sub-plans (own stream, serial)
-    // while the previous block's numeric pass runs on the other.  Sets
-    // *nnz_c; IAS_ERROR_INSUFFICIENT_CAPACITY when C's capacity is exceeded
-    // (nothing written beyond it, *nnz_c = what is needed).
-    ias_plan *pipe[2] = {nullptr, nullptr};
-    ias_status pipelined(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows, int64_t cols,
-                         int64_t a_entries, int64_t *c_ptr, int32_t *c_col, double *c_val, int64_t cap,
-                         int32_t nblocks, int64_t *nnz_c, ias_report *rep);
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
 };

@@ -32,22 +32,9 @@ namespace dev {
 constexpr int WAVE = 64;
 constexpr int32_t EMPTY_KEY = -1;
 
-// Timing-only ablation builds (tools/ablate.sh; never shipped): 1 = no
-// ordering rounds, 2 = no emission, 4 = no B value gather, 8 = no rank scan,
-// 16 = symbolic without hash inserts.
-#ifndef IAS_ABLATE
-#define IAS_ABLATE 0
-#endif
-#ifndef STREAM_NT
-#define STREAM_NT 1
-#endif
 // a read of the expansion (tcol): streamed once per pass
 __device__ __forceinline__ int32_t ld_stream(const int32_t *p) {
-#if STREAM_NT
     return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
 }
 
 // Timing-only builds (-DIAS_TIMING=1, tools/timing.sh; never shipped): per-
@@ -125,7 +112,6 @@ struct AxOut {
     int64_t *bstart;
     int32_t *blen;
     double *aval;
-    int32_t *row;
     int32_t *wide_b;   // nullable: set to 1 when a selected B row ends beyond 2^30 entries
 };
 
@@ -304,9 +290,7 @@ struct Team {
 
 // first-touch bits of a partitioned row staged in LDS by each partition's
 // workgroup (positions < 32 * LBITS_WORDS; later ones go to global atomics)
-#ifndef LBITS_WORDS
-#define LBITS_WORDS 2048
-#endif
+constexpr int LBITS_WORDS = 2048;
 
 // table slot hash (multiply-shift onto [0, size), any size) and an
 // independent partition hash
@@ -459,114 +443,15 @@ __device__ __forceinline__ int load_segment(const AxView &ax, int64_t q0, int32_
 
 // ---------------------------------------------------------------- symbolic
 // K inserts per lane into a keys + first-touch table, one CAS round trip at a
-// time (default).  INSERT_VEC=1 issues the K first-probe CASes back to back
-// (idle items CAS EMPTY over EMPTY at a lane-spread slot: a no-op) and lets
-// only collided items probe on; on MI355X it measured slower (K3' symbolic
-// 8.7 vs 7.6 ms; 12.9 ms when idle items all hit one slot): several
-// returning LDS atomics in flight per wave cost more than they hide.  minp
+// time (measured: issuing the K first-probe CASes back to back was slower,
+// K3' symbolic 8.7 vs 7.6 ms — several returning LDS atomics in flight per
+// wave cost more than they hide).  minp
 // keeps the smallest product per column (atomicMin without return).
 // slot[k] = the column's slot or -1 (none, or table full: *full set).
-#ifndef INSERT_VEC
-#define INSERT_VEC 0
-#endif
 template <int K>
 __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t S, const int32_t (&c)[K],
                                          const uint32_t (&p)[K], bool (&use)[K], int (&slot)[K],
                                          int &created, bool &full) {
-#if INSERT_VEC == 2   // measured 2x slower than one item at a time (K3' symbolic 15.8 vs 7.5 ms)
-    // Bucketed, K items in lockstep: all K bucket reads in flight, then all
-    // needed CASes issued back to back (an item that needs none CASes EMPTY
-    // over EMPTY at a slot of its own bucket: a no-op), then resolution;
-    // rounds repeat only for items whose CAS lost to another column.
-    const uint32_t nb = S >> 2;
-    uint32_t b[K];
-    bool pend[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        pend[k] = use[k];
-        b[k] = use[k] ? slot_hash(c[k], nb) : (uint32_t)(threadIdx.x % nb);
-        slot[k] = -1;
-    }
-    for (uint32_t round = 0; round < S; ++round) {
-        int4 q[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) q[k] = ((const int4 *)key)[b[k]];
-        int tgt[K];
-        bool cas[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            int hit = -1, empty = -1;
-            if (q[k].w == c[k]) hit = 3;
-            if (q[k].z == c[k]) hit = 2;
-            if (q[k].y == c[k]) hit = 1;
-            if (q[k].x == c[k]) hit = 0;
-            if (q[k].w == EMPTY_KEY) empty = 3;
-            if (q[k].z == EMPTY_KEY) empty = 2;
-            if (q[k].y == EMPTY_KEY) empty = 1;
-            if (q[k].x == EMPTY_KEY) empty = 0;
-            if (pend[k] && hit >= 0) {
-                slot[k] = (int)(4 * b[k] + hit);
-                pend[k] = false;
-            }
-            cas[k] = pend[k] && empty >= 0;
-            tgt[k] = cas[k] ? empty : 0;
-        }
-        int32_t v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            v[k] = atomicCAS(&key[4 * b[k] + tgt[k]], EMPTY_KEY, cas[k] ? c[k] : EMPTY_KEY);
-        bool again = false;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (cas[k] && (v[k] == EMPTY_KEY || v[k] == c[k])) {
-                created += v[k] == EMPTY_KEY ? 1 : 0;
-                slot[k] = (int)(4 * b[k] + tgt[k]);
-                pend[k] = false;
-            } else if (pend[k] && !cas[k]) {
-                b[k] = (b[k] + 1u == nb) ? 0u : b[k] + 1u;   // bucket full: next one
-            }
-            again |= pend[k];
-        }
-        if (!again) break;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
-        else if (use[k]) full = true;
-    }
-#elif INSERT_VEC
-    // round 1: every item's home slot, K CASes back to back (an idle item
-    // CASes EMPTY over EMPTY at its own lane's slot: a no-op, no hot spot)
-    uint32_t s[K];
-    int32_t v[K];
-    const uint32_t idle = (uint32_t)(threadIdx.x % S);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        s[k] = use[k] ? slot_hash(c[k], S) : idle;
-        v[k] = atomicCAS(&key[s[k]], EMPTY_KEY, use[k] ? c[k] : EMPTY_KEY);
-    }
-    // collided items probe on one at a time
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        slot[k] = -1;
-        if (!use[k]) continue;
-        uint32_t t = s[k];
-        int32_t w = v[k];
-        for (uint32_t probe = 1; probe <= S; ++probe) {
-            if (w == EMPTY_KEY || w == c[k]) {
-                created += w == EMPTY_KEY ? 1 : 0;
-                slot[k] = (int)t;
-                break;
-            }
-            t = (t + 1u == S) ? 0u : t + 1u;
-            w = atomicCAS(&key[t], EMPTY_KEY, c[k]);
-        }
-        if (slot[k] < 0) full = true;
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
-#else
     // Bucketed probing: the home position is a 16-byte bucket of 4 slots,
     // read with one LDS load; the column is found in it, or CASed into its
     // first empty slot, or the probe moves to the next bucket.  Linear
@@ -608,7 +493,6 @@ __device__ __forceinline__ void insert_k(int32_t *key, uint32_t *minp, uint32_t 
         if (slot[k] >= 0) atomicMin(&minp[slot[k]], p[k]);
         else full = true;
     }
-#endif
 }
 
 // One team counts the distinct columns of one hash partition of a row whose
@@ -831,291 +715,10 @@ __device__ __forceinline__ int32_t symbolic_bucket_row(const uint2 *bk, int32_t 
     return TM::sum(created, scratch);
 }
 
-// ---------------------------------------------------------------- symbolic, streaming rows
-// Symbolic pass of an LDS-bin row (products tcol[ref.q0 .. + ref.n)) that
-// also prepares the table-free numeric pass: keys + first-touch position per
-// distinct column, then
-//   * the row's first-touch bitmap (bit p set iff product p is the first
-//     touch of its column), built in `lbits` (ceil(P/32) words);
-//   * the targets of the row's duplicate products (product index of the
-//     first touch of the same column), in product order, in `dupt`
-//     (at most dcap of them; *ndup = the count, which may exceed dcap).
-// `c` holds the row's first step of columns on entry (loaded by the caller,
-// so the loads overlap earlier work); the last step loads the first step of
-// `next` into it.  Returns the number of distinct columns.
-template <int TEAM, int K>
-__device__ __forceinline__ void load_step(const int32_t *tcol, const RowRef &ref, int p0, int32_t (&c)[K]) {
-    const int lane = Team<TEAM>::lane();
-    const int32_t *pc = tcol + ref.q0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int p = p0 + k * TEAM + lane;
-        c[k] = p < ref.n ? ld_stream(pc + p) : EMPTY_KEY;
-    }
-}
-
-// Clear n 32-bit words at a 16-byte aligned LDS address with 16-byte stores
-// (the caller's allocation covers n rounded up to 4).
-template <int TEAM>
-__device__ __forceinline__ void lds_fill4(uint32_t *a, uint32_t n, uint32_t v) {
-    uint4 *a4 = (uint4 *)a;
-    const uint4 q = make_uint4(v, v, v, v);
-    for (uint32_t i = Team<TEAM>::lane(); i < (n + 3) / 4; i += TEAM) a4[i] = q;
-}
-
-template <int TEAM, int K>
-__device__ __forceinline__ int32_t symbolic_row_st(const int32_t *tcol, const RowRef &ref,
-                                                   const RowRef &next, int32_t (&c)[K],
-                                                   const SymTable<true> &table, int *scratch,
-                                                   uint32_t *lbits, uint32_t nwords, uint2 *dups,
-                                                   uint32_t dcap, uint32_t &ndup, Timer &tm) {
-    using TM = Team<TEAM>;
-    const int lane = TM::lane();
-    const uint32_t S = table.size;
-    const int32_t P = ref.n;
-    constexpr int STEP = TEAM * K;
-    int *dcount = scratch + 60;   // duplicates seen (scratch[0..16) serves the team scans)
-    lds_fill4<TEAM>((uint32_t *)table.key, S, (uint32_t)EMPTY_KEY);
-    lds_fill4<TEAM>(table.minp, S, 0xFFFFFFFFu);
-    lds_fill4<TEAM>(lbits, nwords, 0u);
-    if (lane == 0) *dcount = 0;
-    TM::sync();
-    tm.mark(0);
-    int created = 0;
-    bool full = false;
-    for (int p0 = 0; p0 < P; p0 += STEP) {
-#if IAS_TIMING
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // timing builds: load wait = phase 1
-        tm.mark(1);
-#endif
-        uint32_t pp[K];
-        bool use[K];
-        int slot[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            pp[k] = (uint32_t)(p0 + k * TEAM + lane);
-            use[k] = c[k] != EMPTY_KEY;
-        }
-        insert_k<K>(table.key, table.minp, S, c, pp, use, slot, created, full);
-        // next step's loads (or the next row's first) overlap this step's
-        // barrier and duplicate check
-        if (p0 + STEP < P) load_step<TEAM, K>(tcol, ref, p0 + STEP, c);
-        else load_step<TEAM, K>(tcol, next, 0, c);
-        tm.mark(2);
-        TM::sync();
-        tm.mark(3);
-        // a product is a duplicate when its column was touched first by an
-        // earlier product (final once the step's inserts have synced; later
-        // steps only bring larger products, so no second barrier is needed).
-        // Duplicates are listed unordered; their product-order index comes
-        // from the finished bitmap (d = p - rank(p)).
-        bool ft[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            ft[k] = false;
-            if (slot[k] >= 0) {
-                const uint32_t m = table.minp[slot[k]];
-                ft[k] = m == pp[k];
-                if (!ft[k]) {
-                    const int i = atomicAdd(dcount, 1);
-                    if ((uint32_t)i < dcap) dups[i] = make_uint2(pp[k], m);
-                }
-            }
-        }
-        // first-touch bits straight from ballots (items of one k and one wave
-        // are 64 consecutive products), no scan of the table afterwards
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint64_t bal = __ballot(ft[k]);
-            const uint32_t base = (uint32_t)(p0 + k * TEAM);
-            if constexpr (TEAM >= WAVE) {
-                const uint32_t wb = base + (uint32_t)(lane & ~(WAVE - 1));   // 64-aligned
-                if ((lane & (WAVE - 1)) == 0 && wb < (uint32_t)P) {
-                    lbits[wb >> 5] = (uint32_t)bal;
-                    lbits[(wb >> 5) + 1] = (uint32_t)(bal >> 32);
-                }
-            } else {
-                const int tb = (int)(__lane_id() & ~(TEAM - 1));
-                const uint32_t bits = (uint32_t)((bal >> tb) & ((1ull << TEAM) - 1ull));
-                if (lane == 0 && bits) atomicOr(&lbits[base >> 5], bits << (base & 31));
-            }
-        }
-        tm.mark(4);
-    }
-    TM::sync();
-    ndup = (uint32_t)*dcount;
-    const int32_t n = TM::sum(created, scratch);
-    tm.mark(5);
-    return n;
-}
-
 // ---------------------------------------------------------------- numeric, streaming rows
-// Table-free numeric pass of the streaming rows (symbolic_row_st ran on them
-// and their duplicates fit dcap), flat over A entries: a wave takes FLAT_CHUNK
-// consecutive entries and walks their products with its lanes (load-balanced
-// by products, independent of row boundaries).  A product whose bitmap bit is
-// set is the first touch of its column: rank = set bits before it in the
-// row, and (col, 0.0 + p) goes straight to its final position.  A duplicate's
+// The streaming rows' numeric pass is k_num2 (num2_kernels.hpp); a duplicate's
 // product is parked at dupval[dup_off[row] + d] (d = duplicates before it in
-// the row) for the fix-up pass (numeric_fixup_row).
-constexpr int FLAT_CHUNK = 64;   // entries per wave chunk (== WAVE)
-
-struct FlatArgs {
-    const int32_t *ax_row;     // row of every A entry
-    const int64_t *axp;        // product offset of every A entry (exclusive prefix)
-    const int64_t *poff;       // product offset of every row
-    int64_t n_entries;
-    const int32_t *tcol;       // product columns (expansion)
-    Bitmap bm;
-    const int32_t *dupn;       // per row: duplicates (>= 0) or -1 (table path)
-    const int64_t *dup_off;
-    double *dupval;
-};
-
-struct FlatEntry {
-    int64_t g;        // product offset of the entry
-    int64_t bstart;   // B row start
-    int64_t cbase;    // C position base: order 0 -> start + nnz - 1, order 1 -> start
-    int64_t bmw;      // bitmap word offset of the row
-    int64_t dbase;    // duplicate-value base of the row
-    double aval;
-    int32_t p0;       // row-relative product index of the entry's first product
-    int32_t start;    // chunk-relative index of the entry's first product
-};
-
-// Products of the chunk are mapped to their entries by per-window start
-// masks (see k_expand): the chunk's non-empty entries are compacted into
-// `ent`, each sets the bit of its first product in `masks`, and lane l of a
-// 64-product window belongs to entry ecur + popcount(mask & bits 0..l).
-constexpr int FLAT_MW = 64;
-
-template <int K>
-// FLAT_BCOL=1: the flat numeric reads the product's column from B itself
-// (the line it gathers the value's row from) instead of the expansion.
-#ifndef FLAT_BCOL
-#define FLAT_BCOL 1   // the expansion now covers only the partitioned rows (sym2)
-#endif
-// FLAT_NT=1: C leaves through non-temporal stores (not read back; B's rows
-// keep the caches); STREAM_NT=1: the expansion is written and read the same way.
-#ifndef FLAT_NT
-#define FLAT_NT 1
-#endif
-__device__ __forceinline__ void numeric_flat_chunk(const AxView &ax, const Rows &B, const FlatArgs &fa,
-                                                   const Out &out, int64_t q0, FlatEntry *ent,
-                                                   unsigned long long *masks) {
-    const int lane = (int)(threadIdx.x & (WAVE - 1));
-    const uint64_t upto = (2ull << lane) - 1ull;
-    auto wave_sync = [] {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    const int64_t q = q0 + lane;
-    int len = 0;
-    FlatEntry e{};
-    if (q < fa.n_entries) {
-        const int32_t row = fa.ax_row[q];
-        const int32_t dn = fa.dupn[row];
-        if (dn >= 0) {
-            len = ax.blen[q];
-            e.g = fa.axp[q];
-            e.bstart = ax.bstart[q];
-            e.aval = ax.aval[q];
-            e.p0 = (int32_t)(e.g - fa.poff[row]);
-            const int64_t st = out.start(row);
-            const int32_t nz = out.len[row];
-            e.cbase = out.order == 0 ? st + nz - 1 : st;
-            e.bmw = fa.bm.off[row];
-            e.dbase = fa.dup_off[row];
-        }
-    }
-    // exclusive prefix of the entries' products over the wave
-    int x = len;
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-        const int t = __shfl_up(x, d);
-        if (lane >= d) x += t;
-    }
-    const int T = __shfl(x, WAVE - 1);
-    const int start = x - len;
-    const uint64_t nzb = __ballot(len > 0);
-    if (len > 0) {
-        e.start = start;
-        ent[__popcll(nzb & ((1ull << lane) - 1ull))] = e;
-    }
-    const int sgn = out.order == 0 ? -1 : 1;
-    struct Step {
-        int32_t c[K];
-        double bv[K];
-        uint32_t word[K], pre[K];
-        int ei[K], j[K];
-    };
-    for (int seg0 = 0; seg0 < T; seg0 += WAVE * FLAT_MW) {
-        masks[lane] = 0ull;   // FLAT_MW == WAVE
-        wave_sync();
-        if (len > 0 && start >= seg0 && start < seg0 + WAVE * FLAT_MW)
-            atomicOr(&masks[(start - seg0) >> 6], 1ull << ((start - seg0) & 63));
-        int ecur = __popcll(__ballot(len > 0 && start < seg0)) - 1;
-        wave_sync();
-        const int nwin = min(FLAT_MW, (T - seg0 + WAVE - 1) / WAVE);
-        // Software-pipelined: the loads of window group i+1 are issued before
-        // the stores of group i (vmcnt retires loads and stores in issue
-        // order, so a load issued after a store would also wait for it).
-        auto load = [&](int w0, Step &S) {
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                S.ei[k] = -1;
-                if (w0 + k < nwin) {
-                    const uint64_t m = masks[w0 + k];
-                    const int ei = ecur + __popcll(m & upto);
-                    ecur += __popcll(m);
-                    const int t = seg0 + (w0 + k) * WAVE + lane;
-                    if (t < T) {
-                        const FlatEntry &E = ent[ei];
-                        S.ei[k] = ei;
-                        S.j[k] = t - E.start;
-#if FLAT_BCOL
-                        S.c[k] = B.col[E.bstart + S.j[k]];   // beside the value: same B row
-#else
-                        S.c[k] = ld_stream(fa.tcol + E.g + S.j[k]);
-#endif
-                        S.bv[k] = B.val[E.bstart + S.j[k]];
-                        const uint32_t p = (uint32_t)(E.p0 + S.j[k]);
-                        S.word[k] = fa.bm.bits[E.bmw + (p >> 5)];
-                        S.pre[k] = fa.bm.pref[E.bmw + (p >> 5)];
-                    }
-                }
-            }
-        };
-        Step cur, nxt;
-        load(0, cur);
-        for (int w0 = 0; w0 < nwin; w0 += K) {
-            if (w0 + K < nwin) load(w0 + K, nxt);
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                if (cur.ei[k] < 0) continue;
-                const FlatEntry &E = ent[cur.ei[k]];
-                const double prod = E.aval * cur.bv[k];
-                const uint32_t p = (uint32_t)(E.p0 + cur.j[k]);
-                const uint32_t rk = cur.pre[k] + (uint32_t)__popc(cur.word[k] & ((1u << (p & 31)) - 1u));
-                if ((cur.word[k] >> (p & 31)) & 1u) {
-                    const int64_t pos = E.cbase + sgn * (int64_t)rk;
-#if FLAT_NT
-                    __builtin_nontemporal_store(cur.c[k], &out.col[pos]);
-                    __builtin_nontemporal_store(out.first_assign ? prod : 0.0 + prod, &out.val[pos]);
-#else
-                    out.col[pos] = cur.c[k];
-                    out.val[pos] = out.first_assign ? prod : 0.0 + prod;
-#endif
-                } else {
-                    fa.dupval[E.dbase + (p - rk)] = prod;
-                }
-            }
-            cur = nxt;
-        }
-        wave_sync();
-    }
-}
+// the row) for the fix-up kernels below.
 
 // Fix-up of one streaming row with duplicates: each column's duplicate
 // products are added to its entry in product order (one lane per column).
@@ -1365,7 +968,7 @@ __device__ __forceinline__ void numeric_row(const AxView &ax, const Rows &B, con
             }
 #pragma unroll
             for (int k = 0; k < K; ++k)
-                if (pend[k]) prod[k] = (IAS_ABLATE & 4) ? sg.aval[jj[k]] : sg.aval[jj[k]] * B.val[kk[k]];
+                if (pend[k]) prod[k] = sg.aval[jj[k]] * B.val[kk[k]];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 slot[k] = 0;
@@ -1381,18 +984,16 @@ __device__ __forceinline__ void numeric_row(const AxView &ax, const Rows &B, con
             }
             bool first_round = true;
             while (true) {
-#if !(IAS_ABLATE & 1)
 #pragma unroll
                 for (int k = 0; k < K; ++k)
                     if (pend[k]) t.claim((uint32_t)slot[k], (uint32_t)(k * TEAM + lane));
                 TM::sync();
-#endif
                 bool win[K];
                 M rank[K];
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
                     const M m = pend[k] ? t.load((uint32_t)slot[k]) : (M)0;
-                    win[k] = pend[k] && ((IAS_ABLATE & 1) || (m & MT::OWN) == (M)(k * TEAM + lane));
+                    win[k] = pend[k] && (m & MT::OWN) == (M)(k * TEAM + lane);
                     rank[k] = m >> MT::SHIFT;
                 }
                 bool ft[K];
@@ -1401,7 +1002,7 @@ __device__ __forceinline__ void numeric_row(const AxView &ax, const Rows &B, con
                 if (first_round) {
                     if constexpr (!PART) {
                         int r[K] = {};
-                        const int total = (IAS_ABLATE & 8) ? 0 : TM::template excl_count_items<K>(ft, r, scratch);
+                        const int total = TM::template excl_count_items<K>(ft, r, scratch);
 #pragma unroll
                         for (int k = 0; k < K; ++k)
                             if (ft[k]) rank[k] = (M)(base_rank + (uint32_t)r[k]);
@@ -1448,7 +1049,7 @@ __device__ __forceinline__ void numeric_row(const AxView &ax, const Rows &B, con
     }
     if (full) atomicOr(overflow, 1);
     if constexpr (DW) return;
-    if (row < 0 || (IAS_ABLATE & 2)) return;
+    if (row < 0) return;
     if constexpr (WIDE) {
         const int64_t ow = out.start(row);
         const uint32_t n = base_rank;

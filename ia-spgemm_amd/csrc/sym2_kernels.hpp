@@ -96,7 +96,6 @@ struct Sym2Args {
     int32_t *dupn;
     int32_t *gdupt;
     int32_t dcap;              // duplicate targets allocated per row (dup_off spacing): more -> table path
-    int32_t ablate;            // timing experiments only (IAS_S2_ABLATE): 2 no gathers
     int32_t bm_need;           // heavy rows above this nnz get dupn -3: the numeric pass's
                                // partitioned path needs a bitmap they do not have
     const int32_t *count_dev;  // non-null: the row count is read here (sym3's retry list)
@@ -155,9 +154,7 @@ __device__ __forceinline__ Sym2Row sym2_detail(const Sym2Args &a, const RowRef &
     return r;
 }
 
-#ifndef SYM2_DB_MAX
-#define SYM2_DB_MAX 8   // K up to which a team double-buffers the next row's columns in registers
-#endif
+constexpr int SYM2_DB_MAX = 8; // K up to which a team double-buffers the next row's columns in registers
 
 // range reduction of a 32-bit hash onto [0, n)
 __device__ __forceinline__ uint32_t reduce32(uint32_t h, uint32_t n) {
@@ -272,7 +269,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int p = (k0 + t) * TEAM + lane;
-                c[k0 + t] = (a.ablate & 2) ? p : a.bcol[p < P ? at[t] : 0];
+                c[k0 + t] = a.bcol[p < P ? at[t] : 0];
             }
         }
     };
@@ -353,9 +350,8 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         TM::sync();
         tm.mark(4);
         const int32_t nl = *lcount;
-        if ((uint32_t)nl > L.LC || (a.ablate & 4)) {
+        if ((uint32_t)nl > L.LC) {
             // heavy row: count distinct columns in a keys-only table over f1 .. own
-            // (IAS_S2_ABLATE & 4: every row, an A/B of table-path numeric)
             int32_t *hk = (int32_t *)f1;
             const uint32_t HS = L.heavy_slots();
             for (uint32_t i = lane; i < HS; i += TEAM) hk[i] = EMPTY_KEY;

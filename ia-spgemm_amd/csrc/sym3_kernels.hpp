@@ -174,7 +174,7 @@ __device__ __forceinline__ void s3_gather(const Sym3Args &a, Sym3Lds<K> &L, cons
         const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, k);
         const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mk >> 32), k);
         const uint64_t m = ((uint64_t)hi << 32) | lo;
-        const int e = min(max(c0 + __popcll(m & upto) - 1, 0), WAVE - 1);
+        const int e = min(max(c0 + (int)__popcll(m & upto) - 1, 0), WAVE - 1);   // int: __popcll is unsigned
         eb[k] = L.ebase[e];
         c0 += __popcll(m);
     }

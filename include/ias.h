@@ -254,12 +254,11 @@ ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, const ias_csr *
 ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, const ias_csr *B,
                                    ias_csr *C, int32_t order, ias_report *report);
 
-/* Single-call form on device-resident CSR (no separate nnz call): the fused
- * form of CSR_MUL_CSR's two loops (csr/common_csr.h:95-189).  A with at least
- * 4M entries is cut into row blocks of equal A entries (IAS_PIPE_BLOCKS,
- * default 4; 1 = one block) and each block's symbolic pass runs beside the
- * previous block's numeric pass, C's entries of a block placed after the
- * previous block's; smaller A runs the two-phase engine behind one call.
+/* Single-call form on device-resident CSR (no separate nnz call): the two
+ * loops of CSR_MUL_CSR (csr/common_csr.h:95-189) as the two-phase engine
+ * behind one call.  (A row-block pipeline — each block's symbolic pass beside
+ * the previous block's numeric pass — was measured 4-40% slower on K2/K3/K3'/
+ * K4 and dropped)
  * C->row_ptr
  * (rows+1), C->col and C->val are caller-provided device arrays of capacity
  * C->nnz; nnz(C) <= flops(A*B) (ias_flops), so that capacity always suffices.

@@ -1,7 +1,7 @@
 """Full-size parity on the GPU: the BASELINE.json configurations K1, K2, K3'
 and K3 through the device-resident two-phase C-ABI
-(ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, and the one-call row-block
-pipeline ias_csr_mul_csr_into), checked against the
+(ias_csr_mul_csr_nnz + ias_csr_mul_csr_compute, and the one-call
+ias_csr_mul_csr_into), checked against the
 oracle's CSR_MUL_CSR restatement recorded in tests/golden/generator_stats.json
 by make_generator_stats.py:
 
@@ -48,9 +48,7 @@ def make(rec):
 def device_spgemm(torch, A, order=ias.ORDER_REFERENCE, via="twophase"):
     """C = A*A with A and C in HBM; returns (row_ptr, col, val) torch tensors and
     the symbolic report.  via="twophase": ias_csr_mul_csr_nnz + _compute;
-    via="into": one ias_csr_mul_csr_into call into C of capacity flops(A*A)
-    (the row-block pipeline for large A, each block's symbolic pass beside the
-    previous block's numeric pass)."""
+    via="into": one ias_csr_mul_csr_into call into C of capacity flops(A*A)."""
     dev = torch.device("cuda", 0)
     rp = torch.from_numpy(A.row_ptr).to(dev)
     ci = torch.from_numpy(A.col).to(dev)

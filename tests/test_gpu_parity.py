@@ -28,20 +28,6 @@ def need_gpu():
         pytest.fail("no HIP device visible: the gpu tests must run on an MI355X box")
 
 
-@pytest.fixture(autouse=True)
-def engine(monkeypatch):
-    """Every case runs through the two-phase engine; the row-block pipeline of
-    ias_csr_mul_csr_into (on by default for A of >= 4M entries) has its own
-    cases below, forced onto small inputs (test_pipeline_*)."""
-    monkeypatch.setenv("IAS_PIPE_BLOCKS", "1")
-    return "twophase"
-
-
-def pipeline_on(monkeypatch, blocks=3):
-    monkeypatch.setenv("IAS_PIPE_BLOCKS", str(blocks))
-    monkeypatch.setenv("IAS_PIPE_MIN", "0")
-
-
 def bits(a):
     return np.ascontiguousarray(a, np.float64).view(np.int64)
 
@@ -619,11 +605,8 @@ def chunk_edges(seed=21):
     return ias.HostCsr(n, n, rp, col, val)
 
 
-@pytest.mark.parametrize("pipe", [False, True], ids=["twophase", "pipeline"])
 @pytest.mark.parametrize("which", ["rmat14", "edges", "dups", "long"])
-def test_into_single_call(which, pipe, monkeypatch):
-    if pipe:
-        pipeline_on(monkeypatch, 4)
+def test_into_single_call(which):
     A = {"rmat14": lambda: ias.gen_rmat(14, 16, seed=4), "edges": chunk_edges,
          "dups": lambda: duplicate_tiers()[0], "long": long_rows}[which]()
     B = duplicate_tiers()[1] if which == "dups" else A
@@ -687,41 +670,6 @@ def test_host_operand_transfer_times():
         ias.lib.ias_csr_free(C.byref(c))
     finally:
         ias.lib.ias_csr_free(C.byref(dA))
-
-
-# ------------------------------------------------------------------ row-block pipeline
-def _into_numpy(A, blocks, monkeypatch, order=ias.ORDER_REFERENCE):
-    pipeline_on(monkeypatch, blocks)
-    fl = ob.flops(ob.Mat.of(A), ob.Mat.of(A))
-    dA = _dev(A)
-    plan = C.c_void_p()
-    ias.check(ias.lib.ias_plan_create(C.byref(plan), 0, None), "plan")
-    try:
-        st, dC = _into(plan, dA, dA, A.rows, A.cols, max(fl, 1), order)
-        ias.check(st, "into (pipeline)")
-        got = ias.csr_to_numpy(dC)
-        ias.lib.ias_csr_free(C.byref(dC))
-        return got
-    finally:
-        ias.lib.ias_plan_destroy(plan)
-        ias.lib.ias_csr_free(C.byref(dA))
-
-
-@pytest.mark.parametrize("name", SQUARE)
-def test_pipeline_inputs(inputs_dir, name, monkeypatch):
-    A, _ = ias.mtx_read(os.path.join(inputs_dir, name))
-    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
-    assert_csr_identical(_into_numpy(A, 3, monkeypatch), ref, name + " (pipeline)")
-
-
-@pytest.mark.parametrize("blocks", [2, 5, 64])
-@pytest.mark.parametrize("case", cases_small()[:4], ids=lambda c: c[0])
-def test_pipeline_synthetic(case, blocks, monkeypatch):
-    """Block bounds cut by A's entries: 64 blocks of a small A leave empty
-    blocks (skipped) and one-row blocks."""
-    name, A, _ = case
-    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
-    assert_csr_identical(_into_numpy(A, blocks, monkeypatch), ref, f"{name} (pipeline {blocks})")
 
 
 # ------------------------------------------------------------------ sorted order, wide rows
