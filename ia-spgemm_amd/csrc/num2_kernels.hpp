@@ -98,7 +98,7 @@ __device__ __forceinline__ void st16(void *p, uint4 v) {
 // stores in issue order, so a load behind a store would wait for the store).
 constexpr int N2_K = 4;
 
-constexpr int N2_WPE = 1; // minimum waves per SIMD the register allocation must allow (1: no cap)
+constexpr int N2_WPE = 1;   // minimum waves per SIMD the register allocation must allow (1: no cap)
 __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_WPE))) void k_num2(Num2Args a,
                                                                                                  Out out) {
     constexpr int K = N2_K;
@@ -109,12 +109,8 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     };
     __shared__ Ent ent[N2_WPB][N2_ENT];
     __shared__ unsigned long long wmask[N2_WPB][K];
-    // staged first touches by rank, modulo BUF: a step's entries plus the
-    // carried partial line of the previous step (< 32 columns / 16 values)
-    constexpr int BUF = 2 * PASS;
-    static_assert((BUF & (BUF - 1)) == 0 && BUF >= PASS + 32, "staging ring");
-    __shared__ __attribute__((aligned(16))) int32_t scol[N2_WPB][BUF];
-    __shared__ __attribute__((aligned(16))) double sval[N2_WPB][BUF];
+    __shared__ __attribute__((aligned(16))) int32_t scol[N2_WPB][PASS];
+    __shared__ __attribute__((aligned(16))) double sval[N2_WPB][PASS];
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)(threadIdx.x & (WAVE - 1));
     const int64_t u = (int64_t)blockIdx.x * N2_WPB + w;
@@ -156,12 +152,9 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     const int64_t cbase = out.order == 0 ? cst + nnz - 1 : cst;   // C position of rank 0
     const uint64_t upto = (2ull << lane) - 1ull;                // bits 0..lane
     const uint32_t below = (1u << (lane & 31)) - 1u;
-    // 16-byte pieces start where the destination address is 16-byte aligned;
-    // 128-byte lines (32 columns / 16 values) where it is line aligned
+    // 16-byte pieces start where the destination address is 16-byte aligned
     const int64_t cph = (int64_t)(((uintptr_t)out.col >> 2) & 3u);
     const int64_t vph = (int64_t)(((uintptr_t)out.val >> 3) & 1u);
-    const int64_t cphl = (int64_t)(((uintptr_t)out.col >> 2) & 31u);
-    const int64_t vphl = (int64_t)(((uintptr_t)out.val >> 3) & 15u);
     // rank of the unit's first product = the row's first touches before pa
     int32_t r0;
     {
@@ -198,59 +191,8 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
             S.pre[k] = a.bm.pref[wi];
         }
     };
-    // Stage the step's first touches by rank, park its duplicates, flush.
-    // Only whole 128-byte lines leave at the edge the next step continues
-    // (order 0 writes the unit's C range downwards, order 1 upwards): the
-    // partial line there stays staged and leaves with the next step, so a line
-    // is written by one store pass (measured: a partial line written in two
-    // passes made the L2 fetch it, ~1 GB per launch on K3').  The unit's
-    // last step flushes everything.
-    int32_t fc = r0, fv = r0;   // first rank not yet written: columns, values
-    auto flush = [&](bool is_col, int64_t xa, int64_t xb) {
-        if (xa >= xb) return;
-        auto slot = [&](int64_t x) -> int32_t {
-            const int64_t rk = out.order == 0 ? cbase - x : x - cbase;
-            return (int32_t)(rk & (BUF - 1));
-        };
-        if (is_col) {
-            const int64_t a4 = ((xa + cph + 3) & ~3ll) - cph, e4 = ((xb + cph) & ~3ll) - cph;
-#pragma unroll
-            for (int it = 0; it < ((PASS + 32) / 4 + WAVE - 1) / WAVE; ++it) {   // a step + the carried line
-                const int64_t x = a4 + 4ll * (lane + WAVE * it);
-                if (x + 4 <= e4) {
-                    uint4 v;
-                    v.x = (uint32_t)scol[w][slot(x)];
-                    v.y = (uint32_t)scol[w][slot(x + 1)];
-                    v.z = (uint32_t)scol[w][slot(x + 2)];
-                    v.w = (uint32_t)scol[w][slot(x + 3)];
-                    st16(&out.col[x], v);
-                }
-            }
-            // partial pieces at both ends: lanes 0-2 low, 3-5 high
-            int64_t xc = -1;
-            if (lane < 3) xc = xa + lane < min(a4, xb) ? xa + lane : -1;
-            else if (lane < 6) xc = max(e4, a4) + (lane - 3) < xb ? max(e4, a4) + (lane - 3) : -1;
-            if (xc >= 0) __builtin_nontemporal_store(scol[w][slot(xc)], &out.col[xc]);
-        } else {
-            const int64_t a2 = ((xa + vph + 1) & ~1ll) - vph, e2 = ((xb + vph) & ~1ll) - vph;
-#pragma unroll
-            for (int it = 0; it < ((PASS + 16) / 2 + WAVE - 1) / WAVE; ++it) {
-                const int64_t x = a2 + 2ll * (lane + WAVE * it);
-                if (x + 2 <= e2) {
-                    const double d0 = sval[w][slot(x)], d1 = sval[w][slot(x + 1)];
-                    uint4 v;
-                    __builtin_memcpy(&v.x, &d0, 8);
-                    __builtin_memcpy(&v.z, &d1, 8);
-                    st16(&out.val[x], v);
-                }
-            }
-            int64_t xv = -1;
-            if (lane == 0) xv = xa < min(a2, xb) ? xa : -1;
-            else if (lane == 1) xv = max(e2, a2) < xb ? max(e2, a2) : -1;
-            if (xv >= 0) __builtin_nontemporal_store(sval[w][slot(xv)], &out.val[xv]);
-        }
-    };
-    auto store = [&](int32_t pw0, const Step &S, bool last) {
+    // stage the step's first touches by rank, park its duplicates, flush
+    auto store = [&](int32_t pw0, const Step &S) {
         int nft = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -261,54 +203,69 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
             const int32_t rk = (int32_t)(pre + (uint32_t)__popc(word & below));
             const double prod = ent[w][S.e[k]].av * S.bv[k];
             if (ft) {
-                scol[w][rk & (BUF - 1)] = S.c[k];
-                sval[w][rk & (BUF - 1)] = out.first_assign ? prod : 0.0 + prod;
+                scol[w][rk - r0] = S.c[k];
+                sval[w][rk - r0] = out.first_assign ? prod : 0.0 + prod;
             } else if (in) {
                 a.dupval[dbase + (p - rk)] = prod;
             }
             nft += __popcll(__ballot(ft));
         }
         wave_sync();
-        const int32_t R = r0 + nft;   // ranks staged so far: [fc | fv, R) not yet written
-        if (out.order == 0) {
-            // x = cbase - rank: the unwritten ranks are x in (cbase - R, cbase - f]
-            const int64_t lo = cbase - (R - 1);
-            const int64_t lc = last ? lo : ((lo + cphl + 31) & ~31ll) - cphl;
-            const int64_t lv = last ? lo : ((lo + vphl + 15) & ~15ll) - vphl;
-            flush(true, lc, cbase - fc + 1);
-            flush(false, lv, cbase - fv + 1);
-            fc = max(fc, (int32_t)(cbase - lc + 1));
-            fv = max(fv, (int32_t)(cbase - lv + 1));
-        } else {
-            // x = cbase + rank: the unwritten ranks are x in [cbase + f, cbase + R)
-            const int64_t hi = cbase + R;
-            const int64_t hc = last ? hi : ((hi + cphl) & ~31ll) - cphl;
-            const int64_t hv = last ? hi : ((hi + vphl) & ~15ll) - vphl;
-            flush(true, cbase + fc, hc);
-            flush(false, cbase + fv, hv);
-            fc = max(fc, (int32_t)(hc - cbase));
-            fv = max(fv, (int32_t)(hv - cbase));
+        // C positions of the staged ranks r0 .. r0 + nft - 1: [xlo, xhi)
+        const int64_t xlo = out.order == 0 ? cbase - (r0 + nft - 1) : cbase + r0;
+        const int64_t xhi = xlo + nft;
+        const int64_t i0 = out.order == 0 ? cbase - r0 : -(cbase + r0);
+        auto idx = [&](int64_t x) -> int32_t { return out.order == 0 ? (int32_t)(i0 - x) : (int32_t)(x + i0); };
+        // whole 16-byte pieces: [a4, e4) of the columns, [a2, e2) of the values
+        const int64_t a4 = ((xlo + cph + 3) & ~3ll) - cph, e4 = ((xhi + cph) & ~3ll) - cph;
+        const int64_t a2 = ((xlo + vph + 1) & ~1ll) - vph, e2 = ((xhi + vph) & ~1ll) - vph;
+#pragma unroll
+        for (int it = 0; it < (PASS / 4 + WAVE) / WAVE; ++it) {
+            const int64_t x = a4 + 4ll * (lane + WAVE * it);
+            if (x + 4 <= e4) {
+                uint4 v;
+                v.x = (uint32_t)scol[w][idx(x)];
+                v.y = (uint32_t)scol[w][idx(x + 1)];
+                v.z = (uint32_t)scol[w][idx(x + 2)];
+                v.w = (uint32_t)scol[w][idx(x + 3)];
+                st16(&out.col[x], v);
+            }
         }
-        r0 = R;
+#pragma unroll
+        for (int it = 0; it < (PASS / 2 + WAVE) / WAVE; ++it) {
+            const int64_t x = a2 + 2ll * (lane + WAVE * it);
+            if (x + 2 <= e2) {
+                const double d0 = sval[w][idx(x)], d1 = sval[w][idx(x + 1)];
+                uint4 v;
+                __builtin_memcpy(&v.x, &d0, 8);
+                __builtin_memcpy(&v.z, &d1, 8);
+                st16(&out.val[x], v);
+            }
+        }
+        // the partial pieces at both ends: lanes 0-2 / 3-5 columns, 6 / 7 values
+        int64_t xc = -1, xv = -1;
+        if (lane < 3) xc = xlo + lane < min(a4, xhi) ? xlo + lane : -1;
+        else if (lane < 6) xc = max(e4, a4) + (lane - 3) < xhi ? max(e4, a4) + (lane - 3) : -1;
+        else if (lane == 6) xv = xlo < min(a2, xhi) ? xlo : -1;
+        else if (lane == 7) xv = max(e2, a2) < xhi ? max(e2, a2) : -1;
+        if (xc >= 0) __builtin_nontemporal_store(scol[w][idx(xc)], &out.col[xc]);
+        if (xv >= 0) __builtin_nontemporal_store(sval[w][idx(xv)], &out.val[xv]);
+        r0 += nft;
         wave_sync();
     };
-    // two step buffers, alternating (no register copies between steps); the
-    // next step's gathers are issued before this step's stores, and none past
-    // the unit's last step
+    // two step buffers, alternating (no register copies between steps)
     Step s0, s1;
     int32_t pw0 = (pa >> 6) << 6;
     load(pw0, s0);
     for (;;) {
-        bool last = pw0 + PASS >= pb;
-        if (!last) load(pw0 + PASS, s1);
-        store(pw0, s0, last);
-        if (last) break;
+        load(pw0 + PASS, s1);   // past the unit: clamped, harmless
+        store(pw0, s0);
         pw0 += PASS;
-        last = pw0 + PASS >= pb;
-        if (!last) load(pw0 + PASS, s0);
-        store(pw0, s1, last);
-        if (last) break;
+        if (pw0 >= pb) break;
+        load(pw0 + PASS, s0);
+        store(pw0, s1);
         pw0 += PASS;
+        if (pw0 >= pb) break;
     }
 }
 

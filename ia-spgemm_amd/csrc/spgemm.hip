@@ -1375,7 +1375,7 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
 // sym3's one-wave rows (sym3_kernels.hpp): rows of SYM3_MIN .. SYM3_MAX products
 constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 2048;
 constexpr int SYM3_WPB = 4;
-constexpr int SYM3_DB_MAXK = 8; // K up to which the next row's columns are gathered during a row (registers)
+constexpr int SYM3_DB_MAXK = 4;   // K up to which the next row's columns are gathered during a row (K = 8: 298 vs 309 us on K3')
 template <int K>
 static void sym3_launch(const Sym3Args &a, hipStream_t s) {
     auto kern = k_sym3<K, SYM3_WPB, (K <= SYM3_DB_MAXK)>;

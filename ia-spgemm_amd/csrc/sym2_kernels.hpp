@@ -127,13 +127,24 @@ __device__ __forceinline__ int64_t uni64(int64_t x) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-template <int TEAM>
-__device__ __forceinline__ RowRef sym2_ref(const Sym2Args &a, int64_t idx) {
-    return idx < a.count ? a.list[idx + opaque_zero()] : RowRef{0, -1, 0};
+// The kernel's arguments, read through the kernarg segment where they are
+// used (scalar-cache loads) instead of held in SGPRs across the row loop (as
+// in sym3_kernels.hpp: the loop's hoisted pointer arithmetic spilled).
+typedef const __attribute__((address_space(4))) Sym2Args *S2A;
+__device__ __forceinline__ S2A s2_args() {
+    S2A p = (S2A)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
 }
 
 template <int TEAM>
-__device__ __forceinline__ Sym2Row sym2_detail(const Sym2Args &a, const RowRef &ref) {
+__device__ __forceinline__ RowRef sym2_ref(int32_t count, int64_t idx) {
+    return idx < count ? s2_args()->list[idx + opaque_zero()] : RowRef{0, -1, 0};
+}
+
+template <int TEAM>
+__device__ __forceinline__ Sym2Row sym2_detail(const RowRef &ref) {
+    const S2A a = s2_args();
     Sym2Row r;
     r.ref = ref;
     r.P = 0;
@@ -142,13 +153,13 @@ __device__ __forceinline__ Sym2Row sym2_detail(const Sym2Args &a, const RowRef &
     r.bs = 0;
     if (ref.row >= 0) {
         const int64_t row = (int64_t)ref.row + opaque_zero();
-        r.P = a.prod[row];
-        r.bmoff = a.bm.off[row];
-        r.dupoff = a.dup_off[row];
+        r.P = a->prod[row];
+        r.bmoff = a->bm.off[row];
+        r.dupoff = a->dup_off[row];
         const int lane = Team<TEAM>::lane();
         if (lane < WAVE && lane < ref.n) {
-            r.bl = a.ax.blen[ref.q0 + lane];
-            r.bs = a.ax.bstart[ref.q0 + lane];
+            r.bl = a->ax.blen[ref.q0 + lane];
+            r.bs = a->ax.bstart[ref.q0 + lane];
         }
     }
     return r;
@@ -166,8 +177,7 @@ __device__ __forceinline__ uint32_t fib(int32_t c) { return (uint32_t)c * 0x9E37
 // teams with K >= 16 would otherwise take 160-256 VGPRs, 2 waves per SIMD).
 template <int TEAM, int K, int TPW, int WPE>
 __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))) void k_sym2(Sym2Args a0) {
-    Sym2Args a = a0;
-    if (a0.count_dev) a.count = *a0.count_dev;
+    const int32_t count = a0.count_dev ? *a0.count_dev : a0.count;
     static_assert(TEAM >= WAVE && (TEAM <= WAVE || TPW == 1), "teams are whole waves; multi-wave teams own the WG");
     static_assert(TEAM == WAVE ? K <= 32 : K <= 16, "finish() covers the bitmap words in one pass");
     using TM = Team<TEAM>;
@@ -175,7 +185,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     constexpr int CH = K < 8 ? K : (TEAM > WAVE && K > 8 ? 4 : 8);   // items per register chunk (1024-lane teams: 128 VGPRs)
     constexpr bool DB = K <= SYM2_DB_MAX;      // next row's columns gathered during this row's work
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Sym2Layout L = a.lay;
+    const Sym2Layout L = a0.lay;
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
     unsigned char *base = smem + (size_t)team * L.bytes();
     uint32_t *f1 = (uint32_t *)(base + L.f1());
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     int *scratch = (int *)(base + L.scratch());
     int *lcount = scratch + 60;   // possible duplicates listed (scratch[0..16) serves the team scans)
     int *hcount = scratch + 61;   // heavy rows: distinct columns
-    const int lane = TM::lane();
+    int lane = TM::lane();   // re-hidden every row (below): no lane compares hoisted out of the row loop
     const uint32_t FB = 32u * L.FW;   // filter bits
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -223,8 +233,8 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
                 if (e0 > 0) {
                     bl = 0;
                     if (e0 + lane < n) {
-                        bl = a.ax.blen[q0 + e0 + lane];
-                        bs = a.ax.bstart[q0 + e0 + lane];
+                        bl = s2_args()->ax.blen[q0 + e0 + lane];
+                        bs = s2_args()->ax.bstart[q0 + e0 + lane];
                     }
                 }
                 const int v = bl + (bl > 0 ? (1 << 16) : 0);
@@ -269,7 +279,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int p = (k0 + t) * TEAM + lane;
-                c[k0 + t] = a.bcol[p < P ? at[t] : 0];
+                c[k0 + t] = s2_args()->bcol[p < P ? at[t] : 0];
             }
         }
     };
@@ -448,11 +458,11 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         const int ex = TM::excl_sum(__popc(word), nnz, scratch);
         if (nl < 0) nnz = *hcount;
         // more duplicates than the row's allocated targets: the numeric pass's table path
-        const bool heavy = nl < 0 || P - nnz > a.dcap;
+        const bool heavy = nl < 0 || P - nnz > s2_args()->dcap;
         if ((uint32_t)lane < nw && !heavy) {
             lpref[lane] = (uint32_t)ex;
-            a.bm.bits[bmoff + lane] = word;
-            a.bm.pref[bmoff + lane] = (uint32_t)ex;
+            s2_args()->bm.bits[bmoff + lane] = word;
+            s2_args()->bm.pref[bmoff + lane] = (uint32_t)ex;
         }
         if (nl > 0 && !heavy) {
             TM::sync();   // lpref complete
@@ -465,14 +475,14 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
                     const uint32_t x = (uint32_t)e.x;
                     if (x != (uint32_t)e.y) {
                         const uint32_t rk = lpref[x >> 5] + (uint32_t)__popc(lbits[x >> 5] & ((1u << (x & 31)) - 1u));
-                        a.gdupt[dupoff + (x - rk)] = e.y;
+                        s2_args()->gdupt[dupoff + (x - rk)] = e.y;
                     }
                 }
             }
         }
         if (lane == 0) {
-            a.nnz_row[row] = nnz;
-            a.dupn[row] = heavy ? (nnz > a.bm_need ? -3 : -1) : P - nnz;
+            s2_args()->nnz_row[row] = nnz;
+            s2_args()->dupn[row] = heavy ? (nnz > s2_args()->bm_need ? -3 : -1) : P - nnz;
             *lcount = 0;   // every lane read it before this pass's barriers
         }
         clear_tables();   // the caller's barrier follows
@@ -483,7 +493,7 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
     const int64_t nteams = (int64_t)gridDim.x * TPW;
     int64_t idx = (int64_t)blockIdx.x * TPW + team;
     // the current row (scalars, so nothing of it lives in scratch memory)
-    Sym2Row cur = sym2_detail<TEAM>(a, sym2_ref<TEAM>(a, idx));
+    Sym2Row cur = sym2_detail<TEAM>(sym2_ref<TEAM>(count, idx));
     int32_t row = uni(cur.ref.row), P = uni(cur.P);
     int64_t bmoff = uni64(cur.bmoff), dupoff = uni64(cur.dupoff);
     int32_t c[K];
@@ -492,13 +502,16 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
         gather(P, c);
         TM::sync();   // every wave has read the staging arrays before the loop's stage() rewrites them
     }
-    Sym2Row nxt = sym2_detail<TEAM>(a, sym2_ref<TEAM>(a, idx + nteams));
-    RowRef nref = sym2_ref<TEAM>(a, idx + 2 * nteams);
+    Sym2Row nxt = sym2_detail<TEAM>(sym2_ref<TEAM>(count, idx + nteams));
+    RowRef nref = sym2_ref<TEAM>(count, idx + 2 * nteams);
     tm.start();
     // Software pipeline, per iteration (row i): stage + gather row i+1, its
     // column loads then fly during row i's resolution; prefetch row i+2's
     // details and row i+3's list entry; resolve row i; finish row i.
     while (row >= 0) {
+        // the compiler would otherwise hoist every lane-vs-constant compare of
+        // the loop body out of it and keep the masks in SGPRs (spilled)
+        asm volatile("" : "+v"(lane));
         // row i's columns and row i+1's details have landed (an explicit
         // vmcnt(0) the compiler's wait-count pass sees: the loads issued next
         // are then the only ones in flight)
@@ -511,8 +524,8 @@ __global__ __launch_bounds__(TEAM *TPW) __attribute__((amdgpu_waves_per_eu(WPE))
             tm.mark(1);
             if constexpr (DB) gather(nP, cn);
         }
-        const Sym2Row nn = sym2_detail<TEAM>(a, nref);
-        nref = sym2_ref<TEAM>(a, idx + 3 * nteams);
+        const Sym2Row nn = sym2_detail<TEAM>(nref);
+        nref = sym2_ref<TEAM>(count, idx + 3 * nteams);
         tm.mark(2);
         const int32_t nl = resolve(P, c);
         tm.mark(3);

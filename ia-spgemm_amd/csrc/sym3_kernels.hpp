@@ -81,6 +81,7 @@ struct Sym3Lds {
     __attribute__((aligned(16))) uint32_t f1[F1W];
     __attribute__((aligned(16))) uint32_t f2[F2W];
     int32_t ebase[NE];              // B-row start - first product (B has < 2^30 entries)
+    __attribute__((aligned(8))) uint32_t words[2 * K];   // the classified first-touch words
     unsigned long long mask[K];
     __device__ int2 *list() { return (int2 *)f1; }
     __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
@@ -116,12 +117,27 @@ __device__ __forceinline__ int32_t s3_opaque_zero() {
     return z;
 }
 
+// The kernel's arguments, read through the kernarg segment where they are
+// used (a scalar-cache load each time) rather than held in SGPRs across the
+// row loop: the loop needs every SGPR it has (measured: 105-274 SGPRs spilled
+// to VGPR lanes, a quarter of sym3's VALU instructions in readlane /
+// writelane).  The empty asm hides the pointer's value, so the loads are not
+// hoisted out of the loop.
+typedef const __attribute__((address_space(4))) Sym3Args *S3A;
+__device__ __forceinline__ S3A s3_args() {
+    S3A p = (S3A)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
 // The list entry of row idx (loaded a row ahead of its details, so that no
 // wait for it stalls the loads issued after it).
-__device__ __forceinline__ RowRef s3_ref(const Sym3Args &a, int64_t idx) {
-    return idx < a.count ? a.list[idx + s3_opaque_zero()] : RowRef{0, -1, 0};
+__device__ __forceinline__ RowRef s3_ref(int64_t idx) {
+    const S3A a = s3_args();
+    return idx < a->count ? a->list[idx + s3_opaque_zero()] : RowRef{0, -1, 0};
 }
-__device__ __forceinline__ Sym3Row s3_load(const Sym3Args &a, const RowRef &ref) {
+__device__ __forceinline__ Sym3Row s3_load(const RowRef &ref) {
+    const S3A a = s3_args();
     Sym3Row r;
     r.ref = ref;
     r.P = 0;
@@ -130,13 +146,13 @@ __device__ __forceinline__ Sym3Row s3_load(const Sym3Args &a, const RowRef &ref)
     r.bs = 0;
     if (ref.row >= 0) {
         const int64_t row = (int64_t)ref.row;
-        r.P = a.prod[row];
-        r.bmoff = a.bm.off[row];
-        r.dupoff = a.dup_off[row];
+        r.P = a->prod[row];
+        r.bmoff = a->bm.off[row];
+        r.dupoff = a->dup_off[row];
         const int lane = (int)__lane_id();
         if (lane < ref.n) {
-            r.bl = a.ax.blen[ref.q0 + lane];
-            r.bs = a.ax.bstart[ref.q0 + lane];
+            r.bl = a->ax.blen[ref.q0 + lane];
+            r.bs = a->ax.bstart[ref.q0 + lane];
         }
     }
     return r;
@@ -148,7 +164,7 @@ __device__ __forceinline__ Sym3Row s3_load(const Sym3Args &a, const RowRef &ref)
 // outside the kernel's bounds (P > U, more than 64 entries) is not staged:
 // the caller sends it to the retry list.
 template <int K>
-__device__ __forceinline__ void s3_gather(const Sym3Args &a, Sym3Lds<K> &L, const Sym3Row &r, int32_t (&c)[K]) {
+__device__ __forceinline__ void s3_gather(Sym3Lds<K> &L, const Sym3Row &r, int32_t (&c)[K]) {
     const int lane = (int)__lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
     const bool fits = r.P <= 64 * K && r.ref.n <= WAVE;
@@ -163,24 +179,23 @@ __device__ __forceinline__ void s3_gather(const Sym3Args &a, Sym3Lds<K> &L, cons
         atomicOr(&L.mask[(uint32_t)rel >> 6], 1ull << (rel & 63));
     }
     s3_sync();
-    const unsigned long long mk = lane < K ? L.mask[lane] : 0ull;
     const uint64_t upto = (2ull << lane) - 1ull;
     // every window's entry base first (branch-free LDS reads, one wait), then
-    // every window's column load (all in flight together)
-    int c0 = 0;   // non-empty entries starting before window k (scalar)
+    // every window's column load (all in flight together).  The window masks
+    // are LDS broadcast reads into VGPRs, not readlanes into SGPRs (those
+    // stayed live together and spilled).
+    int c0 = 0;   // non-empty entries starting before window k
     int32_t eb[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mk, k);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mk >> 32), k);
-        const uint64_t m = ((uint64_t)hi << 32) | lo;
+        const uint64_t m = L.mask[k];
         const int e = min(max(c0 + (int)__popcll(m & upto) - 1, 0), WAVE - 1);   // int: __popcll is unsigned
         eb[k] = L.ebase[e];
-        c0 += __popcll(m);
+        c0 += (int)__popcll(m);
     }
     // 32-bit byte offsets from the uniform base (the caller guarantees
     // B.nnz < 2^30): one VGPR per address, the SGPR-base form of the load
-    const char *base = (const char *)a.bcol;
+    const char *base = (const char *)s3_args()->bcol;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         const int p = 64 * k + lane;
@@ -193,7 +208,7 @@ __device__ __forceinline__ void s3_gather(const Sym3Args &a, Sym3Lds<K> &L, cons
 template <int K>
 constexpr int sym3_wpe() { return K <= 8 ? 5 : (K <= 16 ? 4 : 3); }
 template <int K, int WPB, bool DB>
-__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_wpe<K>()))) void k_sym3(Sym3Args a) {
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_wpe<K>()))) void k_sym3(Sym3Args) {
     using LDS = Sym3Lds<K>;
     constexpr int CH = K < 8 ? K : (K % 8 == 0 ? 8 : (K % 6 == 0 ? 6 : 4));   // filter chunk: products per lane whose LDS atomics fly together
     static_assert(K % CH == 0, "K in whole chunks");
@@ -204,7 +219,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
     const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t stride = (int64_t)gridDim.x * WPB;
     int64_t idx = (int64_t)blockIdx.x * WPB + w;
-    if (idx >= a.count) return;
+    if (idx >= s3_args()->count) return;
     for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
     s3_sync();
@@ -215,11 +230,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
     // into the same registers as soon as row i's classification no longer
     // needs them, so they fly during row i's exact phase and finish, and row
     // i+2's details with them.
-    Sym3Row cur = s3_load(a, s3_ref(a, idx));
+    Sym3Row cur = s3_load(s3_ref(idx));
     int32_t c[K];
-    s3_gather<K>(a, L, cur, c);
-    Sym3Row nxt = s3_load(a, s3_ref(a, idx + stride));
-    RowRef nref = s3_ref(a, idx + 2 * stride);
+    s3_gather<K>(L, cur, c);
+    Sym3Row nxt = s3_load(s3_ref(idx + stride));
+    RowRef nref = s3_ref(idx + 2 * stride);
     Timer tm;   // timing builds only (phases: 0 top wait, 1 next row's gather / details issue (DB),
                 // 2 filter, 3 classify + list, 4 exact, 5 finish, 6 filter clear, 7 next row's gather)
     tm.start();
@@ -236,13 +251,18 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
         int32_t cn[DB ? K : 1];
         Sym3Row nn;
         if constexpr (DB) {
-            s3_gather<K>(a, L, nxt, cn);   // nxt.row < 0: dummy loads of B.col[0]
-            nn = s3_load(a, nref);
-            nref = s3_ref(a, idx + 3 * stride);
+            s3_gather<K>(L, nxt, cn);   // nxt.row < 0: dummy loads of B.col[0]
+            nn = s3_load(nref);
+            nref = s3_ref(idx + 3 * stride);
         }
         tm.mark(1);
 
+        // windows holding a product of this lane (64k + lane < P <=> k < nwin),
+        // a VGPR re-derived per phase: one compare per window there, instead of
+        // K window masks the compiler would keep in SGPRs across phases
+        int nwin = (P - lane + 63) >> 6;
         // ---- filter: f1 with return, candidates mark f2 (CH items at a time)
+        asm volatile("" : "+v"(nwin));
         uint32_t candm = 0u;
 #pragma unroll
         for (int k0 = 0; k0 < K; k0 += CH) {
@@ -250,7 +270,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int32_t cc = c[k0 + t];
-                const bool in = 64 * (k0 + t) + lane < P;
+                const bool in = k0 + t < nwin;
                 const uint32_t h = s3_h1(cc, LDS::F1B);
                 bit[t] = in ? 1u << (h & 31) : 0u;
                 old[t] = atomicOr(&L.f1[in ? h >> 5 : 0u], bit[t]);
@@ -272,26 +292,30 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
         uint32_t wd = 0u;   // lane j: bitmap word j
         int32_t nl = 0;
         uint32_t possm = 0u;
+        asm volatile("" : "+v"(nwin));
 #pragma unroll
         for (int k0 = 0; k0 < K; k0 += CH) {
             uint32_t f2w[CH];
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int32_t cc = c[k0 + t];
-                f2w[t] = L.f2[64 * (k0 + t) + lane < P ? s3_h2(cc, LDS::F2B) >> 5 : 0u];
+                f2w[t] = L.f2[k0 + t < nwin ? s3_h2(cc, LDS::F2B) >> 5 : 0u];
             }
 #pragma unroll
             for (int t = 0; t < CH; ++t) {
                 const int k = k0 + t;
                 const int32_t cc = c[k];
-                const bool in = 64 * k + lane < P;
+                const bool in = k < nwin;
                 const bool poss = in && (((candm >> k) & 1u) || ((f2w[t] >> (s3_h2(cc, LDS::F2B) & 31)) & 1u));
                 possm |= (poss ? 1u : 0u) << k;
                 const uint64_t b = __ballot(in && !poss);
-                wd = lane == 2 * k ? (uint32_t)b : (lane == 2 * k + 1 ? (uint32_t)(b >> 32) : wd);
+                // words 2k, 2k+1 via LDS into lanes 2k, 2k+1 after the loop (a
+                // select on lane == 2k kept 2K lane masks live in SGPRs: spills)
+                if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
             }
         }
         s3_sync();   // every f1 / f2 read done before the list overwrites f1
+        wd = lane < 2 * K ? L.words[lane] : 0u;
         int2 *list = L.list();
         int32_t *keys = L.keys();
         uint32_t *own = L.own();
@@ -309,9 +333,9 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
         tm.mark(3);
         if constexpr (!DB) {
             // row i's columns are dead: row i+1's gathers fly from here on
-            s3_gather<K>(a, L, nxt, c);
-            nn = s3_load(a, nref);
-            nref = s3_ref(a, idx + 3 * stride);
+            s3_gather<K>(L, nxt, c);
+            nn = s3_load(nref);
+            nref = s3_ref(idx + 3 * stride);
             tm.mark(7);
         }
         const bool retry = 4 * nl > 3 * LDS::LC || P > LDS::U || nent > WAVE;
@@ -370,11 +394,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
             const int incl = wave_incl_sum((int)cnt);
             const int nnz = __builtin_amdgcn_readlane(incl, WAVE - 1);
             const uint32_t pre = (uint32_t)(incl - (int)cnt);
-            const bool heavy = P - nnz > a.dcap;
+            const bool heavy = P - nnz > s3_args()->dcap;
             if (!heavy) {
                 if (lane < row_nw) {
-                    a.bm.bits[bmoff + lane] = wd;
-                    a.bm.pref[bmoff + lane] = pre;
+                    s3_args()->bm.bits[bmoff + lane] = wd;
+                    s3_args()->bm.pref[bmoff + lane] = pre;
                 }
 #pragma unroll
                 for (int t = 0; t < LDS::LT; ++t) {
@@ -384,13 +408,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
                     const uint32_t pp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((p >> 5) << 2), (int)pre);
                     if (t * WAVE + lane < nl && f[t] != p) {
                         const uint32_t rk = pp + (uint32_t)__popc(pw & ((1u << (p & 31)) - 1u));
-                        a.gdupt[dupoff + (p - rk)] = (int32_t)f[t];
+                        s3_args()->gdupt[dupoff + (p - rk)] = (int32_t)f[t];
                     }
                 }
             }
             if (lane == 0) {
-                a.nnz_row[row] = nnz;
-                a.dupn[row] = heavy ? (nnz > a.bm_need ? -3 : -1) : P - nnz;
+                s3_args()->nnz_row[row] = nnz;
+                s3_args()->dupn[row] = heavy ? (nnz > s3_args()->bm_need ? -3 : -1) : P - nnz;
             }
         } else if (!retry) {
             // ---- finish, no possible duplicate: every product is a first touch
@@ -398,17 +422,17 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
             const int incl = wave_incl_sum((int)cnt);
             const int nnz = __builtin_amdgcn_readlane(incl, WAVE - 1);
             if (lane < row_nw) {
-                a.bm.bits[bmoff + lane] = wd;
-                a.bm.pref[bmoff + lane] = (uint32_t)(incl - (int)cnt);
+                s3_args()->bm.bits[bmoff + lane] = wd;
+                s3_args()->bm.pref[bmoff + lane] = (uint32_t)(incl - (int)cnt);
             }
             if (lane == 0) {
-                a.nnz_row[row] = nnz;
-                a.dupn[row] = P - nnz;
+                s3_args()->nnz_row[row] = nnz;
+                s3_args()->dupn[row] = P - nnz;
             }
         } else if (lane == 0) {
             // outside this kernel's bounds: sym2's teams finish this row
-            const int32_t j = atomicAdd(a.retry_count, 1);
-            a.retry[j] = cref;
+            const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+            s3_args()->retry[j] = cref;
         }
         // ---- the filters empty for the next row
         tm.mark(5);
