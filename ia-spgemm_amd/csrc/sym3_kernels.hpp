@@ -206,7 +206,7 @@ __device__ __forceinline__ void s3_gather(Sym3Lds<K> &L, const Sym3Row &r, int32
 
 // waves per SIMD the register allocation must allow (K columns per lane)
 template <int K>
-constexpr int sym3_wpe() { return K <= 8 ? 5 : (K <= 16 ? 4 : 3); }
+constexpr int sym3_wpe() { return K <= 8 ? 6 : (K <= 12 ? 5 : (K <= 16 ? 4 : 3)); }   // K3': K = 8 289 vs 296 us, K = 12 248 vs 258 us (K = 16 at 5: 211 vs 205)
 template <int K, int WPB, bool DB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_wpe<K>()))) void k_sym3(Sym3Args) {
     using LDS = Sym3Lds<K>;
