@@ -455,14 +455,20 @@ __device__ __forceinline__ RowRef ref_at(const RowRef *list, int64_t idx, int32_
 
 // One workgroup per (row, hash partition): distinct columns of the partition
 // (added to nnz_row) and the first-touch bits of the row's bitmap.
-// Partition buckets: one workgroup per partitioned row reads its expansion
-// once and scatters (column, product) pairs into per-partition buckets
-// (count, scan, scatter in LDS), so that each partition's workgroup reads only
-// its own products instead of rescanning the whole row.  Rows with more than
-// PB_MAXP partitions keep the rescan (span len -1).
+// Partition buckets: one workgroup per partitioned row gathers its products'
+// columns from B (one wave per A entry, lanes along the entry's B row) and
+// scatters (column, product) pairs into per-partition buckets (count, scan,
+// scatter in LDS; the scatter pass gathers again, from the caches), so that
+// each partition's workgroup reads only its own products.  Rows with more
+// than PB_MAXP partitions keep the rescan of their expansion (span len -1;
+// k_expand_part writes it for those rows only).  Measured on K3 (14,470 rows
+// beyond 16,384 products): the expansion pass + a bucket pass over it took
+// 1.28 + 2.58 ms.
 constexpr int PB_BLOCK = 1024;
 constexpr int PB_MAXP = 4096;
-__global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(const int32_t *tcol, const RowRef *list, int32_t count,
+__global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(Rows A, AxView ax, const int64_t *axp,
+                                                          const int64_t *poff, const int32_t *bcol,
+                                                          const RowRef *list, int32_t count,
                                                           const int64_t *pfirst, const int64_t *pboff,
                                                           int32_t part_cap, uint2 *bucket, PartSpan *spans) {
     __shared__ uint32_t cnt[PB_MAXP];
@@ -476,8 +482,14 @@ __global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(const int32_t *tcol, c
         return;
     }
     for (uint32_t q = tid; q < np; q += PB_BLOCK) cnt[q] = 0u;
+    int64_t rs;
+    int32_t ne;
+    A.row(ref.row, rs, ne);
+    const int64_t q0 = rs - A.base();
+    const int64_t p0 = poff[ref.row];
+    const int w = tid / WAVE, lane = tid & (WAVE - 1);
+    constexpr int NW = PB_BLOCK / WAVE;
     __syncthreads();
-    const int32_t *pc = tcol + ref.q0;
     // wave-aggregated LDS atomics: one per (wave, partition present), not per
     // product (a row has few partitions, so per-product atomics all collide)
     const bool direct = np >= 32;   // many partitions: plain LDS atomics rarely collide
@@ -486,43 +498,52 @@ __global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(const int32_t *tcol, c
         uint32_t rank = 0;
         uint64_t todo = __ballot(active);
         while (todo) {
-            const uint32_t q0 = (uint32_t)__shfl((int)q, __builtin_ctzll(todo));
-            const uint64_t same = __ballot(active && q == q0);
+            const uint32_t q1 = (uint32_t)__shfl((int)q, __builtin_ctzll(todo));
+            const uint64_t same = __ballot(active && q == q1);
             const int leader = __builtin_ctzll(same);
             uint32_t base = 0;
-            if (__lane_id() == (uint32_t)leader) base = atomicAdd(&cnt[q0], (uint32_t)__popcll(same));
+            if (__lane_id() == (uint32_t)leader) base = atomicAdd(&cnt[q1], (uint32_t)__popcll(same));
             base = (uint32_t)__shfl((int)base, leader);
-            if (active && q == q0) rank = base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
+            if (active && q == q1) rank = base + (uint32_t)__popcll(same & ((1ull << __lane_id()) - 1ull));
             todo &= ~same;
         }
         return rank;
     };
-    constexpr int U = 4;   // products per thread in flight
-    for (int32_t p0 = 0; p0 < ref.n; p0 += U * PB_BLOCK) {
-        int32_t c[U];
+    // the row's products, entry by entry: U B-row positions per lane in flight
+    constexpr int U = 4;
+    auto sweep = [&](auto &&visit) {
+        for (int32_t e = w; e < ne; e += NW) {
+            const int32_t bl = ax.blen[q0 + e];
+            const int64_t bs = ax.bstart[q0 + e];
+            const int32_t pe = (int32_t)(axp[q0 + e] - p0);
+            for (int32_t j0 = 0; j0 < bl; j0 += U * WAVE) {
+                int32_t c[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t p = p0 + u * PB_BLOCK + tid;
-            c[u] = p < ref.n ? ld_stream(pc + p) : 0;
-        }
+                for (int u = 0; u < U; ++u) {
+                    const int32_t j = j0 + u * WAVE + lane;
+                    c[u] = j < bl ? bcol[bs + j] : 0;
+                }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool act = p0 + u * PB_BLOCK + tid < ref.n;
-            wave_add(act, act ? part_of(c[u], np) : 0u);
+                for (int u = 0; u < U; ++u) {
+                    const int32_t j = j0 + u * WAVE + lane;
+                    visit(j < bl, c[u], pe + j);
+                }
+            }
         }
-    }
+    };
+    sweep([&](bool act, int32_t c, int32_t) { wave_add(act, act ? part_of(c, np) : 0u); });
     __syncthreads();
     // exclusive scan of the counts (np <= PB_MAXP: PB_MAXP / PB_BLOCK per thread)
     constexpr int PER = PB_MAXP / PB_BLOCK;
-    uint32_t v[PER], s = 0;
+    uint32_t v[PER], sum = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const uint32_t q = (uint32_t)(tid * PER + i);
         v[i] = q < np ? cnt[q] : 0u;
-        s += v[i];
+        sum += v[i];
     }
     int tot;
-    const int ex = Team<PB_BLOCK>::excl_sum((int)s, tot, scratch);
+    const int ex = Team<PB_BLOCK>::excl_sum((int)sum, tot, scratch);
     __syncthreads();
     const int64_t base = pboff[ref.row];
     uint32_t run = (uint32_t)ex;
@@ -536,21 +557,10 @@ __global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(const int32_t *tcol, c
         run += v[i];
     }
     __syncthreads();
-    for (int32_t p0 = 0; p0 < ref.n; p0 += U * PB_BLOCK) {
-        int32_t c[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t p = p0 + u * PB_BLOCK + tid;
-            c[u] = p < ref.n ? ld_stream(pc + p) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t p = p0 + u * PB_BLOCK + tid;
-            const bool act = p < ref.n;
-            const uint32_t at = wave_add(act, act ? part_of(c[u], np) : 0u);
-            if (act) bucket[base + at] = make_uint2((uint32_t)c[u], (uint32_t)p);
-        }
-    }
+    sweep([&](bool act, int32_t c, int32_t p) {
+        const uint32_t at = wave_add(act, act ? part_of(c, np) : 0u);
+        if (act) bucket[base + at] = make_uint2((uint32_t)c, (uint32_t)p);
+    });
 }
 
 template <int TEAM, int K, int LOG2S>
@@ -1094,8 +1104,10 @@ __global__ __launch_bounds__(256) void k_wide_gather(const RowRef *list, int32_t
 // columns from B themselves.  Workgroups (row, y) take the row's A entries
 // y*4 + wave, y*4 + wave + 4*gridDim.y, ...; lanes over the entry's B row.
 __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const int64_t *axp, const int64_t *poff,
-                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol) {
+                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol,
+                                                     int32_t part_cap) {
     const RowRef ref = list[blockIdx.x];
+    if (nparts_of(ref.n, part_cap) <= (uint32_t)PB_MAXP) return;   // bucketed from B instead
     int64_t s;
     int32_t n;
     A.row(ref.row, s, n);
@@ -1693,8 +1705,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(lane_no++);
         k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
-                                                               as<int32_t>(bufs[B_TCOL]));
-        k_part_bucket<<<c, PB_BLOCK, 0, t>>>(tcol, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
+                                                               as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
+        k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
                                                  as<PartSpan>(bufs[B_PSPAN]));
         k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
