@@ -59,6 +59,9 @@ def parse(argv=None):
     p.add_argument("--config", default="auto", help="auto | " + " | ".join(CONFIGS))
     p.add_argument("--order", default="reference", choices=["reference", "sorted"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-full", action="store_true",
+                   help="CPU baseline on the full matrix (ILP64 MKL when nnz(C) > 2^31) instead of a row "
+                        "sample for products beyond 1.2e9 flops")
     p.add_argument("--cpu-threads", type=int, default=16)
     p.add_argument("--json-out", default=None)
     p.add_argument("--engine", default="twophase", choices=["twophase", "into"],
@@ -396,7 +399,7 @@ def main(argv=None):
             out["one_shot"] = one_shot(dcsr(0, rows, rp, nnz_a), local, out["ms_per_step"])
         if rank == 0 and world == 1 and as_ranks is None and not args.no_cpu_baseline and \
                 kind in ("rmat", "band", "ell"):
-            out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads, args.cpu_full)
             if out["cpu_baseline"] and out["cpu_baseline"].get("value"):
                 out["speedup_vs_cpu_baseline"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
             out["cpu_baseline_alg2"] = cpu_baseline_alg2(A, flops_total, args.cpu_threads)
@@ -543,8 +546,7 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
     ms_k = statistics.mean(kms)
     rows = int(A.rows)
     alg = 8 * rows * (2 * nda + ndc[0]) + 4 * (2 * nda + ndc[0])   # A, B (= A) read, C written
-    env = os.environ.get("IAS_DIA_MFMA")
-    mfma = env == "1" if env is not None else nda * nda >= 256   # the library's choice (dia.hip)
+    kname = {1: "k_dia_tile", 2: "k_dia_mfma", 3: "k_dia_mul"}.get(int(rep.kernel), "?")   # the library's choice
     out = {
         "metric": METRIC,
         "value": round(2.0 * flops_total / (ms_step * 1e6), 3),
@@ -557,7 +559,7 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
                    "diagonals_a": nda, "diagonals_c": ndc[0], "flops": flops_total, "format": "dia",
                    "parallelism": "single GPU"},
         "roofline": {
-            "kernel": "k_dia_mfma" if mfma else "k_dia_tile",
+            "kernel": kname,
             "bound": "hbm", "achieved": round(alg / (ms_k * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(alg / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
             "alg_bytes_per_launch": alg,
@@ -567,7 +569,7 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
         "setup_s": round(t_gen, 2),
     }
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads, args.cpu_full)
     ias.lib.ias_dia_free(C.byref(da))
     ias.lib.ias_plan_destroy(plan)
     line = json.dumps(out)
@@ -660,18 +662,22 @@ def row_sample(A, every):
                        np.concatenate(cols), np.concatenate(vals))
 
 
-def cpu_baseline(A, flops_total, threads):
+def cpu_baseline(A, flops_total, threads, full=False):
     """The reference's Algorithm 1 (MKL mkl_sparse_sp2m, create+multiply+export
     as main.cpp:746-748) on the host cores: 1 warm-up + median of 3 runs.  The
-    full matrix when its product is small enough for a bounded run; otherwise
-    a row sample (row_sample) times B = A, reported per its own flops."""
+    full matrix when its product is small enough for a bounded run (or with
+    full=True: --cpu-full, ILP64 indices since K3's nnz(C) exceeds 2^31, as the
+    reference's own build needs there); otherwise a row sample (row_sample)
+    times B = A, reported per its own flops."""
     import ias
+    if full:
+        os.environ["IAS_MKL_ILP64"] = "1"   # read when MKL is first loaded (mkl_baseline.cpp)
     ok, ver = ias.mkl_available()
     if not ok:
         return {"value": None, "unit": "GFLOP/s", "cores": 0, "kind": "reference",
                 "sample": "MKL runtime not present on this host"}
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
-    every = 1 if flops_total <= 1_200_000_000 else int(math.ceil(flops_total / 3e8))
+    every = 1 if (full or flops_total <= 1_200_000_000) else int(math.ceil(flops_total / 3e8))
     As = row_sample(A, every)
     f_s = ias.flops(As, A)
     times = []
@@ -689,7 +695,8 @@ def cpu_baseline(A, flops_total, threads):
     return {"value": round(2.0 * f_s / (med * 1e6), 4), "unit": "GFLOP/s", "cores": threads,
             "kind": "reference",
             "sample": f"{what}, MKL mkl_sparse_sp2m FULL_MULT (reference Algorithm 1, "
-                      f"csr/common_csr.h:18-47), {ver.split(' Product')[0]}, LP64, GNU threading, "
+                      f"csr/common_csr.h:18-47), {ver.split(' Product')[0]}, "
+                      f"{'ILP64' if os.environ.get('IAS_MKL_ILP64') == '1' else 'LP64'}, GNU threading, "
                       f"median of 3 after 1 warm-up: {med:.1f} ms",
             "ms": round(med, 2)}
 

@@ -507,6 +507,8 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
             const char *mf = getenv("IAS_DIA_MFMA");
             const bool dense = (int64_t)nda * ndb >= 256 && WA * WC <= 4ll * nda * ndb;
             const bool use_mfma = mfma_ok && (mf ? *mf == '1' : dense);
+            if (rep) rep->kernel = use_mfma ? IAS_DIA_KERNEL_MFMA
+                                            : (small && tile_lds(tr) <= 65536 ? IAS_DIA_KERNEL_TILE : IAS_DIA_KERNEL_PAIRS);
             if (use_mfma) {
                 const int32_t *m = P->d_maps;
                 if (mfma_lds > 65536)

@@ -59,7 +59,16 @@ struct BlockCache {
     std::mutex mu;
     std::map<std::pair<int, size_t>, std::vector<void *>> free;   // (device, size) -> blocks
     std::map<void *, size_t> size_of;                           // cached-class blocks in use or free
+    // freed blocks whose last users may still run: they join `free` after one
+    // device-wide synchronisation, taken when an allocation would reuse them
+    // (one sync per call that allocates, not one per freed array)
+    std::vector<std::pair<void *, size_t>> pending[64];
     size_t held[64] = {};
+    // pending -> free (caller holds the lock and has synchronised the device)
+    void settle(int device) {
+        for (auto &b : pending[device]) free[{device, b.second}].push_back(b.first);
+        pending[device].clear();
+    }
     static size_t round(size_t b) {
         size_t r = 256;
         while (r < b) r <<= 1;
@@ -68,8 +77,10 @@ struct BlockCache {
     // hipFree every cached free block of `device` (caller holds no lock)
     void trim(int device) {
         std::vector<void *> drop;
+        (void)hipDeviceSynchronize();
         {
             std::lock_guard<std::mutex> g(mu);
+            settle(device);
             for (auto it = free.begin(); it != free.end();) {
                 if (it->first.first == device) {
                     for (void *q : it->second) {
@@ -100,13 +111,30 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
     const bool cached = bytes <= BlockCache::MAX_BLOCK && device >= 0 && device < 64;
     const size_t want = cached ? BlockCache::round(bytes) : bytes;
     if (cached) {
-        std::lock_guard<std::mutex> g(c.mu);
-        auto it = c.free.find({device, want});
-        if (it != c.free.end() && !it->second.empty()) {
-            *p = it->second.back();
-            it->second.pop_back();
-            c.held[device] -= want;
-            return IAS_SUCCESS;
+        bool sync = false;
+        {
+            std::lock_guard<std::mutex> g(c.mu);
+            auto it = c.free.find({device, want});
+            if (it != c.free.end() && !it->second.empty()) {
+                *p = it->second.back();
+                it->second.pop_back();
+                c.held[device] -= want;
+                return IAS_SUCCESS;
+            }
+            for (auto &b : c.pending[device]) sync = sync || b.second == want;
+        }
+        if (sync) {
+            // a freed block of this size exists: wait for its last users
+            HIPC(hipDeviceSynchronize());
+            std::lock_guard<std::mutex> g(c.mu);
+            c.settle(device);
+            auto it = c.free.find({device, want});
+            if (it != c.free.end() && !it->second.empty()) {
+                *p = it->second.back();
+                it->second.pop_back();
+                c.held[device] -= want;
+                return IAS_SUCCESS;
+            }
         }
     }
     hipError_t e = hipMalloc(p, want);
@@ -137,11 +165,11 @@ ias_status dev_free(void *p, int device) {
     HIPC(hipSetDevice(device));
     if (keep) {
         // hipFree's ordering: nothing still running may touch the block once
-        // a later call can be handed it
-        HIPC(hipDeviceSynchronize());
+        // a later call is handed it — the block waits in `pending` until an
+        // allocation synchronises the device (dev_alloc)
         std::lock_guard<std::mutex> g(c.mu);
         const size_t r = c.size_of[p];
-        c.free[{device, r}].push_back(p);
+        c.pending[device].push_back({p, r});
         c.held[device] += r;
         return IAS_SUCCESS;
     }

@@ -79,7 +79,7 @@ class Report(C.Structure):
                 ("flops", C.c_int64), ("nnz_c", C.c_int64),
                 ("max_row_products", C.c_int64), ("max_row_nnz", C.c_int64),
                 ("ms_stream", C.c_double), ("stream_products", C.c_int64), ("stream_nnz", C.c_int64),
-                ("stream_launches", C.c_int32), ("reserved1", C.c_int32)]
+                ("stream_launches", C.c_int32), ("kernel", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -145,8 +145,12 @@ typedef struct ias_report {
     int64_t stream_nnz;      /* entries of C it wrote */
     int32_t stream_launches; /* its launches: up to 3 (rows by duplicate class,
                                 each class's fix-ups overlapping the rest) */
-    int32_t reserved1;
+    int32_t kernel;          /* ias_dia_mul_dia: the kernel that ran (IAS_DIA_KERNEL_*) */
 } ias_report;
+/* ias_report.kernel of ias_dia_mul_dia */
+#define IAS_DIA_KERNEL_TILE 1   /* k_dia_tile: LDS row tiles, VALU, bitwise */
+#define IAS_DIA_KERNEL_MFMA 2   /* k_dia_mfma: v_mfma_f64_16x16x4f64 dense blocks */
+#define IAS_DIA_KERNEL_PAIRS 3  /* k_dia_mul: one thread per C element (wide bands) */
 
 typedef struct ias_mtx_info {
     int32_t is_pattern, is_real, is_integer, is_symmetric; /* main.cpp:171-189 */

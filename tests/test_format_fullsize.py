@@ -87,7 +87,9 @@ def _k1_dia(monkeypatch, mfma):
     ias.check(ias.lib.ias_dia_copy(C.byref(hd), C.byref(dd), ias.MEMORY_DEVICE, 0), "upload")
     ias.lib.ias_dia_free(C.byref(hd))
     o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=0)
-    ias.check(ias.lib.ias_dia_mul_dia(C.byref(dd), C.byref(dd), C.byref(dc), C.byref(o), None), "dia")
+    rep = ias.Report()
+    ias.check(ias.lib.ias_dia_mul_dia(C.byref(dd), C.byref(dd), C.byref(dc), C.byref(o), C.byref(rep)), "dia")
+    assert rep.kernel == (2 if mfma else 1), rep.kernel   # IAS_DIA_KERNEL_MFMA / _TILE
     ias.check(ias.lib.ias_dia_copy(C.byref(dc), C.byref(hc), ias.MEMORY_HOST, 0), "download")
     nd = int(hc.num_diagonals)
     got = dict(nd=nd, offsets=ias._np(hc.diagonal_offsets, nd, np.int32),
