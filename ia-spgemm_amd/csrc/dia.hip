@@ -233,9 +233,22 @@ __global__ __launch_bounds__(256) void k_dia_mfma(DiaMfmaArgs a) {
     }
 }
 
-__global__ void k_dia_index(int32_t ndc, const int32_t *offc, int64_t rows, int32_t *ind) {
-    const int32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d < ndc) ind[offc[d] + rows - 1] = d;
+// C's offsets (a copy of the plan's) and diagonal_ind in one pass:
+// ind[o + rows - 1] = the C diagonal of offset o, 0 elsewhere (offc ascending,
+// binary search) — one launch instead of a copy, a memset and a scatter.
+__global__ void k_dia_meta(int32_t ndc, const int32_t *offc, int64_t rows, int64_t span, int32_t *offs,
+                           int32_t *ind) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < ndc) offs[i] = offc[i];
+    if (i >= span) return;
+    const int64_t o = i - (rows - 1);
+    int32_t lo = 0, hi = ndc;   // first d with offc[d] >= o
+    while (lo < hi) {
+        const int32_t m = (lo + hi) >> 1;
+        if (offc[m] < o) lo = m + 1;
+        else hi = m;
+    }
+    ind[i] = (lo < ndc && offc[lo] == o) ? lo : 0;
 }
 
 }  // namespace dev
@@ -474,16 +487,18 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     IAS_TRY(dev_alloc((void **)&D.diagonal_offsets, 4 * (size_t)ndc, device));
     IAS_TRY(dev_alloc((void **)&D.diagonal_ind, 4 * (size_t)span, device));
     IAS_TRY(dev_alloc((void **)&D.val, 8 * (size_t)A->rows * ndc, device));
-    if (ndc) HIPC(hipMemcpyAsync(D.diagonal_offsets, P->d_offc, 4 * (size_t)ndc, hipMemcpyDeviceToDevice, s));
-    if (span) HIPC(hipMemsetAsync(D.diagonal_ind, 0, 4 * (size_t)span, s));
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (rep) dia_events(device, &e0, &e1);
     if (e0) HIPC(hipEventRecord(e0, s));
     const int64_t n = A->rows * (int64_t)ndc;
     const int32_t nda = A->num_diagonals, ndb = B->num_diagonals, np = (int32_t)P->pja.size();
+    if (span > 0 || ndc > 0) {
+        const int64_t m = std::max<int64_t>(span, ndc);
+        dev::k_dia_meta<<<(unsigned)((m + 255) / 256), 256, 0, s>>>(ndc, P->d_offc, A->rows, span,
+                                                                    D.diagonal_offsets, D.diagonal_ind);
+    }
     if (ndc > 0) {
-        dev::k_dia_index<<<(ndc + 255) / 256, 256, 0, s>>>(ndc, D.diagonal_offsets, A->rows, D.diagonal_ind);
         if (n > 0) {
             const int32_t *t = P->d_tab;
             const int32_t lo_a = P->lo_a, span_a = P->span_a, lo_b = P->lo_b, span_b = P->span_b;

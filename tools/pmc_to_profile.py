@@ -1,28 +1,49 @@
 #!/usr/bin/env python3
-"""Turn a tools/pmc_summary.py --json output into profiles/pmc_<config>_n<N>.json,
-the file bench.py reads roofline.traffic from (HBM bytes per launch of the
-roofline kernel, k_numeric_flat).
+"""Per-kernel PMC means (rocprofv3 --pmc CSVs under <root>/pmc_*) ->
+profiles/pmc_<config>_n<N>.json, the file bench.py reads roofline.traffic and
+lds_bank_conflict_ratio from.
 
-FETCH_SIZE / WRITE_SIZE are KiB in rocprofv3.  MI355X_MICROARCH.md (HBM):
-FETCH_SIZE reports half the bytes of a wide coalesced *16-B-per-lane* stream;
-other access widths are uncalibrated.  k_numeric_flat reads with 4- and 8-byte
-lanes (product columns, gathered B values, bitmap words), so the raw counter
-is used for `hbm_bytes_per_launch` and the x2 figure is kept beside it.
+FETCH_SIZE / WRITE_SIZE are KiB.  Calibrated on this GPU with
+tools/fetch_probe.hip (profiles/r03/fetch_probe.txt): every 128-B read
+request beyond L2 is tallied as 64 B, for 4-, 8- and 16-byte lanes alike
+(4 GiB streamed: FETCH_SIZE = 2.097e6 KiB, TCC_EA0_RDREQ = 2^25 = 4 GiB / 128 B),
+so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 4- and 16-byte
+stores.  `hbm_bytes_per_launch` = 2 x FETCH + WRITE: bytes beyond L2 (the
+Infinity Cache may still serve part of the reads).
 
-usage: tools/pmc_to_profile.py summary.json out.json [source-note]
+usage: tools/pmc_to_profile.py <root> out.json [note]
 """
+import collections
+import csv
+import glob
 import json
+import os
+import re
 import sys
 
-summ = json.load(open(sys.argv[1]))
-out = {"source": sys.argv[3] if len(sys.argv) > 3 else sys.argv[1]}
-for k, m in summ.items():
-    if "FETCH_SIZE" not in m or "WRITE_SIZE" not in m:
-        continue
-    fetch = 1024.0 * m["FETCH_SIZE"]
-    write = 1024.0 * m["WRITE_SIZE"]
-    out[k] = {"hbm_bytes_per_launch": round(fetch + write), "fetch_bytes_raw": round(fetch),
-              "fetch_bytes_x2": round(2 * fetch), "write_bytes": round(write),
-              "dur_us": round(m.get("dur_us", 0.0), 1), "l2_hit": m.get("l2_hit")}
-json.dump(out, open(sys.argv[2], "w"), indent=1)
-print(json.dumps(out.get("k_numeric_flat", {})))
+root, dst = sys.argv[1], sys.argv[2]
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in sorted(glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
+    for row in csv.DictReader(open(f)):
+        k = re.sub(r"\(.*", "", row["Kernel_Name"]).replace("void ", "").replace("ias::dev::", "")
+        vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+out = {"source": sys.argv[3] if len(sys.argv) > 3 else root,
+       "calibration": "read bytes = 2 x FETCH_SIZE (tools/fetch_probe.hip); WRITE_SIZE exact"}
+lds = {}
+for k, cs in sorted(vals.items()):
+    m = {c: sum(v) / len(v) for c, v in cs.items()}
+    e = {}
+    if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+        fetch, write = 2 * 1024.0 * m["FETCH_SIZE"], 1024.0 * m["WRITE_SIZE"]
+        e.update(hbm_bytes_per_launch=round(fetch + write), read_bytes=round(fetch), write_bytes=round(write),
+                 fetch_size_kib_raw=round(m["FETCH_SIZE"], 1))
+    if "TCC_HIT_sum" in m and "TCC_MISS_sum" in m and m["TCC_HIT_sum"] + m["TCC_MISS_sum"] > 0:
+        e["l2_hit"] = round(m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"]), 4)
+    if m.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
+        e["lds_bank_conflict_ratio"] = round(m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"], 4)
+        lds[k] = e["lds_bank_conflict_ratio"]
+    if e:
+        out[k] = e
+out["lds_bank_conflict_ratio"] = lds
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out.get("k_num2", {})))
