@@ -6,6 +6,7 @@
 #include "spgemm_kernels.hpp"
 #include "sym2_kernels.hpp"
 #include "sym3_kernels.hpp"
+#include "sym4_kernels.hpp"
 #include "num2_kernels.hpp"
 #include <functional>
 #include "short_kernels.hpp"
@@ -1385,7 +1386,7 @@ static void sym2_bin(int cfg, const Sym2Args &a, hipStream_t s) {
 
 
 // sym3's one-wave rows (sym3_kernels.hpp): rows of SYM3_MIN .. SYM3_MAX products
-constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 2048;
+constexpr int32_t SYM3_MIN = 257, SYM3_MAX = 2048;   // sym4<2048> on 1,025 - 2,048: 0.98 vs 0.79 ms (K3', serial)
 constexpr int SYM3_WPB = 4;
 constexpr int SYM3_DB_MAXK = 4;   // K up to which the next row's columns are gathered during a row (K = 8: 298 vs 309 us on K3')
 template <int K>
@@ -1408,6 +1409,26 @@ static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream
     retry.count_dev = a.retry_count;
     if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
     else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
+}
+
+// sym4's one-wave long rows (sym4_kernels.hpp): rows of SYM3_MAX+1 .. SYM4_MAX
+// products; the rows it hands back go to the bin's own sym2 teams.  K3'
+// serial: 2,049 - 4,096 products 0.89 ms (sym2's 512-lane teams 1.2 ms);
+// 4,097 - 8,192 1.0 ms (sym2's 1024-lane teams 0.96 ms: kept).
+constexpr int32_t SYM4_MAX = 4096;
+constexpr int SYM4_WPB = 2;
+template <int U>
+static void sym4_launch(const Sym3Args &a, hipStream_t s) {
+    auto kern = k_sym4<U, 16, 8, SYM4_WPB>;
+    const int64_t want = ((int64_t)a.count + SYM4_WPB - 1) / SYM4_WPB;
+    const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM4_WPB, 0));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM4_WPB, 0, s>>>(a);
+}
+static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+    retry.list = a.retry;
+    retry.count_dev = a.retry_count;   // retry.count (the bin's rows) bounds the grid
+    sym4_launch<SYM4_MAX>(a, s);
+    sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s);   // the 2,049 - 4,096 bins' team (cfg 6)
 }
 
 template <int TEAM, int K, int SEG, int TPW, int PER>
@@ -1729,10 +1750,18 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             }
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
                         sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
+            if (!c1.wide_b && u > SYM3_MAX && u <= SYM4_MAX) {
+                const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                                  &dc->s3_retry[b & 15]};
+                sym4_bin(a4, a2, t);
+                CHECK_LAUNCH("k_sym4", t);
+                continue;
+            }
             if (!c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
                 const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
-                                  &dc->s3_retry[b & 7]};   // a counter per bin (bins run concurrently)
+                                  &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
                 Sym2Args r2 = a2;
                 r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
                 sym3_bin(u, a3, r2, t);

@@ -1,0 +1,348 @@
+// sym4_kernels.hpp — symbolic pass of the long rows (2,049 .. U products),
+// one wave per row, the row's products in chunks of 64*KC.
+//
+// Restates CSR_MUL_CSR's first loop (IA-SPGEMM-CPU_release/detail/csr/
+// common_csr.h:95-125: distinct columns per row) and the discovery order of
+// its second loop (:133-189), producing what sym2 / sym3 produce for the
+// table-free numeric pass: nnz, the row's first-touch bitmap + word prefixes,
+// and each duplicate's first-touch product.
+//
+// sym3 (sym3_kernels.hpp) keeps a row's columns in registers (K per lane) and
+// its entries one per lane, so it stops at 2,048 products (K = 32: 168 VGPRs,
+// 3 waves per SIMD).  Here the columns never stay in registers beyond a chunk:
+//   * the row's entries (up to U/16) are staged in groups of 64 — per entry
+//     its B-row base in LDS and its start bit in the per-window start masks;
+//   * filter pass (per chunk: gather, f1 ORs with return, candidates mark
+//     f2; the chunk's candidate bits go to LDS as one ballot per window);
+//   * classify pass (per chunk: the same gathers again — the row's columns
+//     are L2 / Infinity-Cache resident by then — f2 reads, one ballot per
+//     window gives the certain first touches, the possible duplicates are
+//     listed over the dead f1);
+//   * exact pass over the list and finish as in sym3, with the bitmap words
+//     and their prefixes in LDS.
+// Rows beyond the kernel's bounds, or whose list overflows, go to the retry
+// list that sym2's teams finish.  Measured against sym2's 512 / 1024-lane
+// teams on K3': see DESIGN.md §4.
+#pragma once
+
+#include "sym3_kernels.hpp"
+
+namespace ias {
+namespace dev {
+
+template <int U, int F1BPP>
+struct Sym4Lds {
+    static constexpr int NWIN = U / 64;            // 64-product windows
+    static constexpr int F1B = F1BPP * U;          // f1 bits
+    static constexpr int F1W = F1B / 32;
+    static constexpr int F2B = 2 * U;              // f2 bits
+    static constexpr int F2W = F2B / 32;
+    static constexpr int BW = U / 32;              // bitmap words
+    static constexpr int NE = U / 32;              // A entries per row at most
+    static constexpr int LC = U * F1BPP / 128;     // possible-duplicate list (8 B each) +
+    static constexpr int ES = LC;                  //   exact table (8 B per slot) = f1's bytes
+    static constexpr int LT = LC / WAVE;           // list entries per lane
+    static constexpr int WPL = BW / WAVE;          // bitmap words per lane in the finish scan
+    static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
+    static_assert(BW % WAVE == 0 && LC % WAVE == 0 && NE % WAVE == 0, "whole waves");
+    __attribute__((aligned(16))) uint32_t f1[F1W];
+    __attribute__((aligned(16))) uint32_t f2[F2W];
+    unsigned long long smask[NWIN];                // entry start bits per window
+    union {
+        unsigned long long cand[NWIN];             // candidate bits per window (filter, classify)
+        uint32_t pref[BW];                         // exclusive prefixes of the bitmap words (finish)
+    };
+    int32_t ebase[NE];                             // B-row start - first product, per non-empty entry
+    uint32_t words[BW];                            // first-touch bitmap
+    __device__ int2 *list() { return (int2 *)f1; }
+    __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
+    __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
+};
+
+constexpr int SYM4_WPE = 4;   // waves per SIMD the registers must allow (LDS allows 3.5 at U = 4096)
+template <int U, int F1BPP, int KC, int WPB>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_WPE))) void k_sym4(Sym3Args) {
+    using LDS = Sym4Lds<U, F1BPP>;
+    __shared__ LDS lds[WPB];
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
+    const int lane = (int)__lane_id();
+    LDS &L = lds[w];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t upto = (2ull << lane) - 1ull;   // lane 63: all ones
+    const int64_t stride = (int64_t)gridDim.x * WPB;
+    int64_t idx = (int64_t)blockIdx.x * WPB + w;
+    if (idx >= s3_args()->count) return;
+    for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
+    s3_sync();
+
+    // a row's details: its list entry, products, and the B-row extents of its
+    // first 64 entries (prefetched a row ahead)
+    struct Det {
+        RowRef ref;
+        int32_t P, bl;
+        int64_t bs;
+    };
+    auto details = [&](const RowRef &r) {
+        Det d{r, 0, 0, 0};
+        if (r.row >= 0) {
+            d.P = s3_args()->prod[r.row];
+            if (lane < r.n) {
+                d.bl = s3_args()->ax.blen[r.q0 + lane];
+                d.bs = s3_args()->ax.bstart[r.q0 + lane];
+            }
+        }
+        return d;
+    };
+    Det cur = details(s3_ref(idx));
+    for (; idx < s3_args()->count; idx += stride) {
+        const RowRef ref = cur.ref;
+        const int32_t row = __builtin_amdgcn_readfirstlane(ref.row);
+        const int32_t E = __builtin_amdgcn_readfirstlane(ref.n);
+        const int32_t P = __builtin_amdgcn_readfirstlane(cur.P);
+        const RowRef nref = s3_ref(idx + stride);
+        if (P > U || E > LDS::NE) {   // outside this kernel's bounds: sym2's teams finish it
+            if (lane == 0) {
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
+            }
+            cur = details(nref);
+            continue;
+        }
+        const int64_t q0 = ref.q0;
+        const int nwin = (P + 63) >> 6;
+        for (int k = lane; k < nwin; k += WAVE) L.smask[k] = 0ull;
+        s3_sync();
+        // ---- stage the entries, 64 at a time
+        {
+            int carry = 0, nec = 0;
+            for (int g = 0; g < E; g += WAVE) {
+                const int e = g + lane;
+                int32_t bl = cur.bl;
+                int64_t bs = cur.bs;
+                if (g > 0) {
+                    bl = 0;
+                    bs = 0;
+                    if (e < E) {
+                        bl = s3_args()->ax.blen[q0 + e];
+                        bs = s3_args()->ax.bstart[q0 + e];
+                    }
+                }
+                const int incl = wave_incl_sum(bl);
+                const int rel = carry + incl - bl;
+                const uint64_t nem = __ballot(bl > 0);
+                if (bl > 0 && rel < P) {
+                    L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
+                    atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
+                }
+                carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
+                nec += (int)__popcll(nem);
+            }
+        }
+        s3_sync();
+        // columns of windows k0 .. k0+KC-1 (c0: non-empty entries starting
+        // before window k0, advanced past the chunk).  Windows beyond the row
+        // and lanes beyond P read B.col[0] (callers mask them): branch-free, so
+        // the wait for a chunk's loads counts exactly the loads issued after it.
+        const char *base = (const char *)s3_args()->bcol;
+        auto gather = [&](int k0, int32_t(&c)[KC], int &c0) {
+            int32_t eb[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const uint64_t m = L.smask[min(k0 + t, LDS::NWIN - 1)];
+                const bool inw = k0 + t < nwin;
+                const int e = min(max(c0 + (int)__popcll(m & upto) - 1, 0), LDS::NE - 1);
+                eb[t] = L.ebase[e];
+                c0 += inw ? (int)__popcll(m) : 0;
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int p = 64 * (k0 + t) + lane;
+                const uint32_t off = p < P ? (uint32_t)(eb[t] + p) << 2 : 0u;
+                c[t] = *(const int32_t *)(base + off);
+            }
+        };
+        // two chunk buffers: chunk j+1's gathers fly while chunk j is worked on
+        auto sweep = [&](auto &&work) {
+            int c0 = 0;
+            int32_t ca[KC], cb[KC];
+            gather(0, ca, c0);
+            for (int k0 = 0; k0 < nwin; k0 += 2 * KC) {
+                gather(k0 + KC, cb, c0);
+                work(k0, ca);
+                if (k0 + KC >= nwin) break;
+                gather(k0 + 2 * KC, ca, c0);
+                work(k0 + KC, cb);
+            }
+        };
+        // ---- filter pass
+        sweep([&](int k0, const int32_t(&c)[KC]) {
+            uint32_t old[KC], bit[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool in = 64 * (k0 + t) + lane < P;
+                const uint32_t h = s3_h1(c[t], LDS::F1B);
+                bit[t] = in ? 1u << (h & 31) : 0u;
+                old[t] = atomicOr(&L.f1[in ? h >> 5 : 0u], bit[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool cand = (old[t] & bit[t]) != 0u;
+                if (cand) {
+                    const uint32_t h = s3_h2(c[t], LDS::F2B);
+                    atomicOr(&L.f2[h >> 5], 1u << (h & 31));
+                }
+                const uint64_t cb = __ballot(cand);
+                if (lane == 0 && k0 + t < nwin) L.cand[k0 + t] = cb;
+            }
+        });
+        // the next row's details fly during the rest of this one
+        const Det nxt = details(nref);
+        s3_sync();   // f1 dead from here: the list overlays it
+        // ---- classify pass: certain first touches -> bitmap words, possible
+        // duplicates -> list (product order)
+        int nl = 0;
+        int2 *list = L.list();
+        sweep([&](int k0, const int32_t(&c)[KC]) {
+            uint32_t f2w[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool in = 64 * (k0 + t) + lane < P;
+                f2w[t] = L.f2[in ? s3_h2(c[t], LDS::F2B) >> 5 : 0u];
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int k = k0 + t;
+                const int p = 64 * k + lane;
+                const bool in = p < P;
+                const uint64_t cm = L.cand[min(k, LDS::NWIN - 1)];
+                const bool poss =
+                    in && (((cm >> lane) & 1ull) || ((f2w[t] >> (s3_h2(c[t], LDS::F2B) & 31)) & 1u));
+                const uint64_t b = __ballot(in && !poss);
+                if (lane == 0 && k < nwin) *(uint64_t *)&L.words[2 * k] = b;
+                const uint64_t pb = __ballot(poss);
+                if (poss) {
+                    const int i = nl + (int)__popcll(pb & lt);
+                    if (i < LDS::LC) list[i] = make_int2(c[t], p);
+                }
+                nl += (int)__popcll(pb);
+            }
+        });
+        s3_sync();
+        const bool retry = 4 * nl > 3 * LDS::LC;
+        if (retry) {
+            if (lane == 0) {
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
+            }
+        } else {
+            // ---- exact: claim the column (CAS, linear probing); its smallest
+            // product is the first touch
+            int2 e[LDS::LT];
+            uint32_t slot[LDS::LT], f[LDS::LT];
+#pragma unroll
+            for (int t = 0; t < LDS::LT; ++t) {
+                e[t] = make_int2(0, -1);
+                slot[t] = 0;
+                f[t] = 0;
+            }
+            if (nl > 0) {
+                int32_t *keys = L.keys();
+                uint32_t *own = L.own();
+                for (int i = lane; i < LDS::ES; i += WAVE) keys[i] = EMPTY_KEY;
+                s3_sync();
+                uint32_t wonm = 0u;
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t) {
+                    const int i = t * WAVE + lane;
+                    if (i < nl) {
+                        e[t] = list[i];
+                        uint32_t s = s3_h3(e[t].x, LDS::ES);
+                        bool won = false;
+                        for (int probe = 0; probe < LDS::ES; ++probe) {
+                            const int32_t g = atomicCAS(&keys[s], EMPTY_KEY, e[t].x);
+                            if (g == EMPTY_KEY) {
+                                won = true;
+                                break;
+                            }
+                            if (g == e[t].x) break;
+                            s = s + 1u == (uint32_t)LDS::ES ? 0u : s + 1u;
+                        }
+                        slot[t] = s;
+                        if (won) own[s] = (uint32_t)e[t].y;
+                        wonm |= (won ? 1u : 0u) << t;
+                    }
+                }
+                s3_sync();
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t)
+                    if (t * WAVE + lane < nl && !((wonm >> t) & 1u)) atomicMin(&own[slot[t]], (uint32_t)e[t].y);
+                s3_sync();
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t) {
+                    if (t * WAVE + lane < nl) {
+                        f[t] = own[slot[t]];
+                        const uint32_t p = (uint32_t)e[t].y;
+                        if (f[t] == p) atomicOr(&L.words[p >> 5], 1u << (p & 31));
+                    }
+                }
+                s3_sync();
+            }
+            // ---- finish: nnz, word prefixes (lane-contiguous words), bitmap
+            const int W = (P + 31) >> 5;
+            uint32_t cnt = 0u;
+#pragma unroll
+            for (int j = 0; j < LDS::WPL; ++j) {
+                const int wi = lane * LDS::WPL + j;
+                cnt += wi < W ? (uint32_t)__popc(L.words[wi]) : 0u;
+            }
+            const int incl = wave_incl_sum((int)cnt);
+            const int nnz = __builtin_amdgcn_readlane(incl, WAVE - 1);
+            {
+                uint32_t run = (uint32_t)(incl - (int)cnt);
+#pragma unroll
+                for (int j = 0; j < LDS::WPL; ++j) {
+                    const int wi = lane * LDS::WPL + j;
+                    if (wi < W) {
+                        L.pref[wi] = run;
+                        run += (uint32_t)__popc(L.words[wi]);
+                    }
+                }
+            }
+            s3_sync();
+            const bool heavy = P - nnz > s3_args()->dcap;
+            if (!heavy) {
+                const int64_t bmoff = s3_args()->bm.off[row];
+                for (int wi = lane; wi < W; wi += WAVE) {
+                    s3_args()->bm.bits[bmoff + wi] = L.words[wi];
+                    s3_args()->bm.pref[bmoff + wi] = L.pref[wi];
+                }
+                if (nl > 0) {
+                    const int64_t dupoff = s3_args()->dup_off[row];
+#pragma unroll
+                    for (int t = 0; t < LDS::LT; ++t) {
+                        const uint32_t p = (uint32_t)e[t].y;
+                        if (t * WAVE + lane < nl && f[t] != p) {
+                            const uint32_t rk =
+                                L.pref[p >> 5] + (uint32_t)__popc(L.words[p >> 5] & ((1u << (p & 31)) - 1u));
+                            s3_args()->gdupt[dupoff + (p - rk)] = (int32_t)f[t];
+                        }
+                    }
+                }
+            }
+            if (lane == 0) {
+                s3_args()->nnz_row[row] = nnz;
+                s3_args()->dupn[row] = heavy ? (nnz > s3_args()->bm_need ? -3 : -1) : P - nnz;
+            }
+        }
+        // ---- the filters empty for the next row
+        s3_sync();
+        for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
+        s3_sync();
+        cur = nxt;
+    }
+}
+
+}  // namespace dev
+}  // namespace ias
