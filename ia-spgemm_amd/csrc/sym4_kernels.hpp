@@ -95,6 +95,8 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         return d;
     };
     Det cur = details(s3_ref(idx));
+    Timer tm;   // timing builds only (phases: 0 staging, 1 filter, 2 classify, 3 exact, 4 finish, 5 clear)
+    tm.start();
     for (; idx < s3_args()->count; idx += stride) {
         const RowRef ref = cur.ref;
         const int32_t row = __builtin_amdgcn_readfirstlane(ref.row);
@@ -175,6 +177,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 work(k0 + KC, cb);
             }
         };
+        tm.mark(0);
         // ---- filter pass
         sweep([&](int k0, const int32_t(&c)[KC]) {
             uint32_t old[KC], bit[KC];
@@ -198,6 +201,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         });
         // the next row's details fly during the rest of this one
         const Det nxt = details(nref);
+        tm.mark(1);
         s3_sync();   // f1 dead from here: the list overlays it
         // ---- classify pass: certain first touches -> bitmap words, possible
         // duplicates -> list (product order)
@@ -229,6 +233,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
             }
         });
         s3_sync();
+        tm.mark(2);
         const bool retry = 4 * nl > 3 * LDS::LC;
         if (retry) {
             if (lane == 0) {
@@ -288,6 +293,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 }
                 s3_sync();
             }
+            tm.mark(3);
             // ---- finish: nnz, word prefixes (lane-contiguous words), bitmap
             const int W = (P + 31) >> 5;
             uint32_t cnt = 0u;
@@ -336,12 +342,16 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
             }
         }
         // ---- the filters empty for the next row
+        tm.mark(4);
         s3_sync();
         for (int i = lane; i < LDS::F1W / 4; i += WAVE) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
         for (int i = lane; i < LDS::F2W; i += WAVE) L.f2[i] = 0u;
         s3_sync();
+        tm.mark(5);
+        tm.done();
         cur = nxt;
     }
+    tm.flush(27, lane == 0);
 }
 
 }  // namespace dev

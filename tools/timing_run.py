@@ -51,6 +51,8 @@ def main():
             kind, team = "sym3 K=%d" % (8, 12, 16)[slot - 24], 64
         elif slot >= 30:
             kind, team = ("onepass" if slot == 31 else "op-big"), 512
+        elif slot == 27:
+            kind, team = "sym4", 64
         elif slot == 29:
             kind, team = "sym-part", 1024
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
