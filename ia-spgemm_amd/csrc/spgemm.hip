@@ -41,9 +41,10 @@ __device__ __forceinline__ int bin_of(const BinSpec &sp, int32_t k, int32_t prod
     if (k <= 0) return 0;
     if (stv == -3) return sp.nval + 2;
     if (stv == -5 && sp.short_base > 0) return sp.short_base + (prod <= 64 ? 0 : (prod <= 128 ? 1 : 2));
-    if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), longer (sorted)
+    if (stv >= 0 && sp.nst > 0) {   // fix-up bins: <= 16 (one lane), <= 256 (one wave), then the
+                                    // sorted fix-ups by list length: <= 1024, <= 4096, longer
         if (stv == 0) return 0;
-        return sp.nval + 3 + sp.ndw + (stv > 256 ? 2 : (stv > 16 ? 1 : 0));
+        return sp.nval + 3 + sp.ndw + (stv > 4096 ? 4 : (stv > 1024 ? 3 : (stv > 256 ? 2 : (stv > 16 ? 1 : 0))));
     }
     if (sp.wide_min > 0 && k >= sp.wide_min) return sp.nval + 2;
     const bool val_class =
@@ -1252,17 +1253,17 @@ static BinSpec num_spec() {
     for (int i = 0; i < N_VAL; ++i) s.upper[i + 1] = VAL_BINS[i].upper;
     for (int i = 0; i < N_DW; ++i) s.upper[N_VAL + 3 + i] = DW_BINS[i].upper;
     // streaming rows: the rows that need a duplicate fix-up (by list length)
-    s.nst = 3;
+    s.nst = 5;
     s.ratio_num = 3;   // value tables when products * 2 > nnz * 3
     s.ratio_den = 2;
     s.part_cap = NUM_PART_CAP;
     s.wide_min = WIDE_MIN;
     s.ft = 0;
     s.zero_nnz = 0;
-    s.short_base = N_VAL + 3 + N_DW + 3;   // after the fix-up bins
+    s.short_base = N_VAL + 3 + N_DW + 5;   // after the fix-up bins
     return s;
 }
-static_assert(N_VAL + 3 + N_DW + 3 + 3 <= MAX_BINS, "short bins beyond MAX_BINS");
+static_assert(N_VAL + 3 + N_DW + 5 + 3 <= MAX_BINS, "short bins beyond MAX_BINS");
 
 // Rows of at most SHORT_MAX products take the short path (short_kernels.hpp:
 // one wave per row, exact LDS table, no bitmap) in both passes.
@@ -1908,22 +1909,23 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         // beside the pass they would starve), the others on the next side
         // stream once their class's units are done, beside the later units
         const int fb = ns.nval + 3 + N_DW;
-        const bool fixups = num_count[fb] + num_count[fb + 1] + num_count[fb + 2] > 0;
+        const bool fixups = num_count[fb] + num_count[fb + 1] + num_count[fb + 2] + num_count[fb + 3] +
+                                num_count[fb + 4] > 0;
         // part 0: lists > 4096 (1024 lanes, whole CUs); 1: 1025 .. 4096; 2: the
         // rest; 3: all
         launch_fix = [&, fb](hipStream_t f, int part) -> ias_status {
             int cf;
-            if ((part == 0 || part == 3) && (cf = num_count[fb + 2]) > 0) {
+            if ((part == 0 || part == 3) && (cf = num_count[fb + 4]) > 0) {
                 static bool fb_done = false;
                 allow_lds(k_fixup_big, fb_done, FIXBIG_LDS);
-                k_fixup_big<<<cf, 1024, FIXBIG_LDS, f>>>(NL + st[fb + 2], cf, bm, sa.dup_off, sa.dupn, sa.dupt,
+                k_fixup_big<<<cf, 1024, FIXBIG_LDS, f>>>(NL + st[fb + 4], cf, bm, sa.dup_off, sa.dupn, sa.dupt,
                                                          as<double>(bufs[B_DUPV]), out);
                 CHECK_LAUNCH("k_fixup_big", f);
             }
-            if ((part == 1 || part == 3) && (cf = num_count[fb + 2]) > 0) {
+            if ((part == 1 || part == 3) && (cf = num_count[fb + 3]) > 0) {
                 static bool fl_done = false;
                 allow_lds(k_fixup_large, fl_done, FIXLARGE_LDS);
-                k_fixup_large<<<cf, 256, FIXLARGE_LDS, f>>>(NL + st[fb + 2], cf, bm, sa.dup_off, sa.dupn,
+                k_fixup_large<<<cf, 256, FIXLARGE_LDS, f>>>(NL + st[fb + 3], cf, bm, sa.dup_off, sa.dupn,
                                                             sa.dupt, as<double>(bufs[B_DUPV]), out);
                 CHECK_LAUNCH("k_fixup_large", f);
             }
