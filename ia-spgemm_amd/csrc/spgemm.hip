@@ -7,6 +7,7 @@
 #include "sym2_kernels.hpp"
 #include "sym3_kernels.hpp"
 #include "sym4_kernels.hpp"
+#include "sym5_kernels.hpp"
 #include "num2_kernels.hpp"
 #include <functional>
 #include "short_kernels.hpp"
@@ -1432,6 +1433,26 @@ static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
     sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s);   // the 2,049 - 4,096 bins' team (cfg 6)
 }
 
+// sym5 (sym5_kernels.hpp): SYM4_MAX+1 .. SYM5_MAX products, NW waves per row
+constexpr int32_t SYM5_MAX = 16384;
+template <int U, int NW>
+static void sym5_launch(const Sym3Args &a, hipStream_t s) {
+    auto kern = k_sym5<U, NW, 8>;
+    const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
+}
+static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+    retry.list = a.retry;
+    retry.count_dev = a.retry_count;
+    if (upper <= 8192) {
+        sym5_launch<8192, 2>(a, s);
+        sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s);    // the bins' team (cfg 7)
+    } else {
+        sym5_launch<16384, 4>(a, s);
+        sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s);   // SYM2_CFG_WIDE
+    }
+}
+
 template <int TEAM, int K, int SEG, int TPW, int PER>
 static void val_launch(const Launch &l, const Out &out) {
     auto kern = k_numeric_val<TEAM, K, SEG, TPW, PER>;
@@ -1751,6 +1772,14 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             }
             Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
                         sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
+            if (!c1.wide_b && u > SYM4_MAX && u <= SYM5_MAX) {
+                const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                                  &dc->s3_retry[b & 15]};
+                sym5_bin(u, a5, a2, t);
+                CHECK_LAUNCH("k_sym5", t);
+                continue;
+            }
             if (!c1.wide_b && u > SYM3_MAX && u <= SYM4_MAX) {
                 const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],

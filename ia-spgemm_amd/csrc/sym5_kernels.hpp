@@ -1,0 +1,327 @@
+// sym5_kernels.hpp — symbolic pass of the long rows (4,097 .. U products):
+// sym4's algorithm (sym4_kernels.hpp) with NW waves per row.
+//
+// Restates CSR_MUL_CSR's first loop (IA-SPGEMM-CPU_release/detail/csr/
+// common_csr.h:95-125) and the discovery order of its second loop (:133-189),
+// producing what sym2 / sym3 / sym4 produce for the table-free numeric pass:
+// nnz, the first-touch bitmap + word prefixes, each duplicate's first touch.
+//
+// One workgroup of NW waves per row, the row's filters shared in LDS.  Wave 0
+// stages the entries (B-row bases, per-window start masks) and the per-window
+// count of entries starting before it, so every window's product -> entry map
+// is self-contained and the waves take the windows in chunks of KC, round
+// robin, each double-buffering its gathers.  Filter and classify are sym4's;
+// the possible duplicates are listed through an LDS counter (any order: the
+// exact pass keeps the smallest product per column), the word prefixes are a
+// workgroup scan.  A row of 8,192 products is resolved by two waves in about
+// the time one wave takes for 4,096 (sym4), with the filters' LDS shared.
+// Rows beyond the bounds or whose list overflows go to the retry list (sym2).
+#pragma once
+
+#include "sym3_kernels.hpp"
+
+namespace ias {
+namespace dev {
+
+template <int U, int NW>
+struct Sym5Lds {
+    static constexpr int T = WAVE * NW;
+    static constexpr int NWIN = U / 64;
+    static constexpr int F1B = 16 * U;             // f1 bits (16 per product)
+    static constexpr int F1W = F1B / 32;
+    static constexpr int F2B = 2 * U;
+    static constexpr int F2W = F2B / 32;
+    static constexpr int BW = U / 32;
+    static constexpr int NE = U / 32;              // A entries per row at most
+    static constexpr int LC = U / 8;               // list (8 B per entry) + exact table (8 B per slot) = f1
+    static constexpr int ES = LC;
+    static constexpr int LT = LC / T;              // list entries per thread
+    static constexpr int WPL = BW / T;             // bitmap words per thread in the finish scan
+    static constexpr int WIN_PL = NWIN / WAVE;     // windows per lane in wave 0's window scan
+    static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
+    static_assert(LC % T == 0 && BW % T == 0 && NWIN % WAVE == 0, "whole workgroups");
+    __attribute__((aligned(16))) uint32_t f1[F1W];
+    __attribute__((aligned(16))) uint32_t f2[F2W];
+    unsigned long long smask[NWIN];                // entry start bits per window
+    union {
+        unsigned long long cand[NWIN];             // candidate bits per window
+        uint32_t pref[BW];                         // word prefixes (finish)
+    };
+    int32_t cbase[NWIN];                           // non-empty entries starting before each window
+    int32_t ebase[NE];
+    uint32_t words[BW];
+    int32_t nl;                                    // list counter
+    int32_t scratch[NW];
+    __device__ int2 *list() { return (int2 *)f1; }
+    __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
+    __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
+};
+
+template <int U, int NW, int KC>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void k_sym5(Sym3Args) {
+    using LDS = Sym5Lds<U, NW>;
+    using TM = Team<LDS::T>;
+    constexpr int T = LDS::T;
+    __shared__ LDS L;
+    const int tid = (int)threadIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
+    const int lane = (int)__lane_id();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t upto = (2ull << lane) - 1ull;
+    for (int i = tid; i < LDS::F1W / 4; i += T) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int i = tid; i < LDS::F2W; i += T) L.f2[i] = 0u;
+
+    for (int64_t idx = blockIdx.x; idx < s3_args()->count; idx += gridDim.x) {
+        const RowRef ref = s3_args()->list[idx];
+        const int32_t row = __builtin_amdgcn_readfirstlane(ref.row);
+        const int32_t E = __builtin_amdgcn_readfirstlane(ref.n);
+        const int32_t P = __builtin_amdgcn_readfirstlane(s3_args()->prod[row]);
+        if (P > U || E > LDS::NE) {
+            if (tid == 0) {
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
+            }
+            continue;
+        }
+        const int nwin = (P + 63) >> 6;
+        const int64_t q0 = ref.q0;
+        if (tid == 0) L.nl = 0;
+        // ---- wave 0: entries -> ebase + start masks, then the window bases
+        if (w == 0) {
+            for (int k = lane; k < nwin; k += WAVE) L.smask[k] = 0ull;
+            s3_sync();
+            int carry = 0, nec = 0;
+            for (int g = 0; g < E; g += WAVE) {
+                const int e = g + lane;
+                int32_t bl = 0;
+                int64_t bs = 0;
+                if (e < E) {
+                    bl = s3_args()->ax.blen[q0 + e];
+                    bs = s3_args()->ax.bstart[q0 + e];
+                }
+                const int incl = wave_incl_sum(bl);
+                const int rel = carry + incl - bl;
+                const uint64_t nem = __ballot(bl > 0);
+                if (bl > 0 && rel < P) {
+                    L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
+                    atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
+                }
+                carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
+                nec += (int)__popcll(nem);
+            }
+            s3_sync();
+            // window bases: lane j takes windows j*WIN_PL .. +WIN_PL
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < LDS::WIN_PL; ++i) {
+                const int k = lane * LDS::WIN_PL + i;
+                cnt += k < nwin ? (int)__popcll(L.smask[k]) : 0;
+            }
+            int run = wave_incl_sum(cnt) - cnt;
+#pragma unroll
+            for (int i = 0; i < LDS::WIN_PL; ++i) {
+                const int k = lane * LDS::WIN_PL + i;
+                if (k < nwin) {
+                    L.cbase[k] = run;
+                    run += (int)__popcll(L.smask[k]);
+                }
+            }
+        }
+        __syncthreads();
+        const char *base = (const char *)s3_args()->bcol;
+        auto gather = [&](int k0, int32_t(&c)[KC]) {
+            int32_t eb[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int k = min(k0 + t, LDS::NWIN - 1);
+                const uint64_t m = L.smask[k];
+                const int e = min(max(L.cbase[k] + (int)__popcll(m & upto) - 1, 0), LDS::NE - 1);
+                eb[t] = L.ebase[e];
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int p = 64 * (k0 + t) + lane;
+                const uint32_t off = p < P ? (uint32_t)(eb[t] + p) << 2 : 0u;
+                c[t] = *(const int32_t *)(base + off);
+            }
+        };
+        // this wave's chunks w, w + NW, ... of KC windows; two buffers
+        auto sweep = [&](auto &&work) {
+            constexpr int STEP = NW * KC;
+            int32_t ca[KC], cb[KC];
+            int k0 = w * KC;
+            gather(k0, ca);
+            for (; k0 < nwin; k0 += 2 * STEP) {
+                gather(k0 + STEP, cb);
+                work(k0, ca);
+                if (k0 + STEP >= nwin) break;
+                gather(k0 + 2 * STEP, ca);
+                work(k0 + STEP, cb);
+            }
+        };
+        // ---- filter
+        sweep([&](int k0, const int32_t(&c)[KC]) {
+            uint32_t old[KC], bit[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool in = 64 * (k0 + t) + lane < P;
+                const uint32_t h = s3_h1(c[t], LDS::F1B);
+                bit[t] = in ? 1u << (h & 31) : 0u;
+                old[t] = atomicOr(&L.f1[in ? h >> 5 : 0u], bit[t]);
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool cand = (old[t] & bit[t]) != 0u;
+                if (cand) {
+                    const uint32_t h = s3_h2(c[t], LDS::F2B);
+                    atomicOr(&L.f2[h >> 5], 1u << (h & 31));
+                }
+                const uint64_t cb = __ballot(cand);
+                if (lane == 0 && k0 + t < nwin) L.cand[k0 + t] = cb;
+            }
+        });
+        __syncthreads();   // f1 dead: the list overlays it
+        // ---- classify
+        int2 *list = L.list();
+        sweep([&](int k0, const int32_t(&c)[KC]) {
+            uint32_t f2w[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const bool in = 64 * (k0 + t) + lane < P;
+                f2w[t] = L.f2[in ? s3_h2(c[t], LDS::F2B) >> 5 : 0u];
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int k = k0 + t;
+                const int p = 64 * k + lane;
+                const bool in = p < P;
+                const uint64_t cm = L.cand[min(k, LDS::NWIN - 1)];
+                const bool poss =
+                    in && (((cm >> lane) & 1ull) || ((f2w[t] >> (s3_h2(c[t], LDS::F2B) & 31)) & 1u));
+                const uint64_t b = __ballot(in && !poss);
+                if (lane == 0 && k < nwin) *(uint64_t *)&L.words[2 * k] = b;
+                const uint64_t pb = __ballot(poss);
+                if (pb) {
+                    int at = 0;
+                    if (lane == 0) at = atomicAdd(&L.nl, (int)__popcll(pb));
+                    at = __shfl(at, 0);
+                    const int i = at + (int)__popcll(pb & lt);
+                    if (poss && i < LDS::LC) list[i] = make_int2(c[t], p);
+                }
+            }
+        });
+        __syncthreads();
+        const int32_t nl = L.nl;
+        if (4 * nl > 3 * LDS::LC) {
+            if (tid == 0) {
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
+            }
+        } else {
+            int2 e[LDS::LT];
+            uint32_t slot[LDS::LT], f[LDS::LT];
+#pragma unroll
+            for (int t = 0; t < LDS::LT; ++t) {
+                e[t] = make_int2(0, -1);
+                slot[t] = 0;
+                f[t] = 0;
+            }
+            if (nl > 0) {
+                int32_t *keys = L.keys();
+                uint32_t *own = L.own();
+                for (int i = tid; i < LDS::ES; i += T) keys[i] = EMPTY_KEY;
+                __syncthreads();
+                uint32_t wonm = 0u;
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t) {
+                    const int i = t * T + tid;
+                    if (i < nl) {
+                        e[t] = list[i];
+                        uint32_t s = s3_h3(e[t].x, LDS::ES);
+                        bool won = false;
+                        for (int probe = 0; probe < LDS::ES; ++probe) {
+                            const int32_t g = atomicCAS(&keys[s], EMPTY_KEY, e[t].x);
+                            if (g == EMPTY_KEY) {
+                                won = true;
+                                break;
+                            }
+                            if (g == e[t].x) break;
+                            s = s + 1u == (uint32_t)LDS::ES ? 0u : s + 1u;
+                        }
+                        slot[t] = s;
+                        if (won) own[s] = (uint32_t)e[t].y;
+                        wonm |= (won ? 1u : 0u) << t;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t)
+                    if (t * T + tid < nl && !((wonm >> t) & 1u)) atomicMin(&own[slot[t]], (uint32_t)e[t].y);
+                __syncthreads();
+#pragma unroll
+                for (int t = 0; t < LDS::LT; ++t) {
+                    if (t * T + tid < nl) {
+                        f[t] = own[slot[t]];
+                        const uint32_t p = (uint32_t)e[t].y;
+                        if (f[t] == p) atomicOr(&L.words[p >> 5], 1u << (p & 31));
+                    }
+                }
+                __syncthreads();
+            }
+            // ---- finish: nnz and word prefixes (thread-contiguous words)
+            const int W = (P + 31) >> 5;
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < LDS::WPL; ++j) {
+                const int wi = tid * LDS::WPL + j;
+                cnt += wi < W ? __popc(L.words[wi]) : 0;
+            }
+            int nnz;
+            const int ex = TM::excl_sum(cnt, nnz, L.scratch);
+            {
+                uint32_t run = (uint32_t)ex;
+#pragma unroll
+                for (int j = 0; j < LDS::WPL; ++j) {
+                    const int wi = tid * LDS::WPL + j;
+                    if (wi < W) {
+                        L.pref[wi] = run;
+                        run += (uint32_t)__popc(L.words[wi]);
+                    }
+                }
+            }
+            __syncthreads();
+            const bool heavy = P - nnz > s3_args()->dcap;
+            if (!heavy) {
+                const int64_t bmoff = s3_args()->bm.off[row];
+                for (int wi = tid; wi < W; wi += T) {
+                    s3_args()->bm.bits[bmoff + wi] = L.words[wi];
+                    s3_args()->bm.pref[bmoff + wi] = L.pref[wi];
+                }
+                if (nl > 0) {
+                    const int64_t dupoff = s3_args()->dup_off[row];
+#pragma unroll
+                    for (int t = 0; t < LDS::LT; ++t) {
+                        const uint32_t p = (uint32_t)e[t].y;
+                        if (t * T + tid < nl && f[t] != p) {
+                            const uint32_t rk =
+                                L.pref[p >> 5] + (uint32_t)__popc(L.words[p >> 5] & ((1u << (p & 31)) - 1u));
+                            s3_args()->gdupt[dupoff + (p - rk)] = (int32_t)f[t];
+                        }
+                    }
+                }
+            }
+            if (tid == 0) {
+                s3_args()->nnz_row[row] = nnz;
+                s3_args()->dupn[row] = heavy ? (nnz > s3_args()->bm_need ? -3 : -1) : P - nnz;
+            }
+        }
+        // ---- the filters empty for the next row
+        __syncthreads();
+        for (int i = tid; i < LDS::F1W / 4; i += T) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = tid; i < LDS::F2W; i += T) L.f2[i] = 0u;
+        __syncthreads();
+    }
+}
+
+}  // namespace dev
+}  // namespace ias
