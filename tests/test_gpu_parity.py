@@ -167,6 +167,46 @@ def duplicate_tiers(seed=11):
     return csr(arows, len(brows)), csr(brows, ncols)
 
 
+def long_row_tiers(seed=5):
+    """Rows for the one-wave / few-wave long-row symbolic kernels (sym4: 2,049 -
+    4,096 products, sym5: 4,097 - 16,384), each with few duplicates, with a
+    possible-duplicate list beyond the kernel's (handed to sym2's teams), and
+    with more entries than sym4 stages (200 entries of 15 columns).  Each tier:
+    (products, B-row length, column pool)."""
+    rng = np.random.default_rng(seed)
+    plan = [(3000, 100, 90000), (3000, 100, 5000), (3000, 15, 90000), (4000, 100, 2500),
+            (6000, 100, 200000), (6000, 100, 9000), (8000, 100, 400000), (8000, 100, 6000),
+            (12000, 100, 500000), (12000, 100, 20000), (16000, 100, 700000), (16000, 100, 12000)]
+    brows, arows = [], []
+    for prods, per, pool in plan:
+        base = len(brows)
+        for _ in range(prods // per):
+            brows.append(rng.choice(pool, per, replace=False))
+        arows.append(np.arange(base, len(brows)))
+    nb = len(brows)
+    for _ in range(3000):
+        brows.append(rng.choice(50000, 20, replace=False))
+    for _ in range(500):   # ordinary rows beside them (sym3 / short)
+        arows.append(rng.choice(np.arange(nb, len(brows)), int(rng.integers(4, 60)), replace=False))
+
+    def csr(rows, ncol):
+        rp = np.zeros(len(rows) + 1, np.int64)
+        rp[1:] = np.cumsum([len(r) for r in rows])
+        col = np.concatenate(rows).astype(np.int32)
+        val = rng.uniform(-1.0, 1.0, size=col.size)
+        return ias.HostCsr(len(rows), ncol, rp, col, val)
+
+    return csr(arows, len(brows)), csr(brows, 700000)
+
+
+def test_csr_long_row_tiers():
+    A, B = long_row_tiers()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    got, rep = ias.spgemm(A, B)
+    assert rep.max_row_products == 16000
+    assert_csr_identical(got, ref, "long-row tiers")
+
+
 def test_csr_duplicate_tiers():
     A, B = duplicate_tiers()
     ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
