@@ -1074,6 +1074,75 @@ __global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_
 // Rows beyond the LDS bins: gathered into a compact workspace (their binning
 // slots), sorted there by one segmented radix sort over all of them (every
 // workgroup of the chip works on them, not one per row), scattered back.
+// Sort of a long row by a column bitmap (C's columns are distinct within a
+// row): every entry sets its column's bit in LDS, a prefix of popcounts (per
+// 8 words) gives each column its sorted position, entries land there in the
+// row's slot of a compact workspace and are copied back.  O(n + cols/32) per
+// row against the segmented radix sort's passes over its keys.  Columns below
+// SORTBM_COLS (the bitmap: 128 KB of LDS + 16 KB of prefixes).
+constexpr int SORTBM_T = 1024;
+constexpr int32_t SORTBM_COLS = 1 << 20;
+constexpr size_t sortbm_lds(int32_t cols) {
+    return 4ull * (((size_t)cols + 255) / 256 * 8) + 4ull * (((size_t)cols + 255) / 256 + 1) + 4ull * 64;
+}
+__global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, int32_t count, const int64_t *ws_off,
+                                                         const int64_t *ptr, const int32_t *len, int64_t stride,
+                                                         int32_t *col, double *val, int32_t ncols, int32_t *wcol,
+                                                         double *wval) {
+    extern __shared__ uint32_t sbm[];
+    const int NW = (ncols + 255) / 256 * 8;   // bitmap words, a multiple of 8
+    uint32_t *bits = sbm;
+    int32_t *pre8 = (int32_t *)(bits + NW);    // exclusive popcount prefix per 8 words
+    int *scratch = pre8 + NW / 8 + 1;
+    const int tid = (int)threadIdx.x;
+    const int per = (NW + SORTBM_T - 1) / SORTBM_T;   // words per thread, a multiple of 8 when NW > T * 8
+    for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        int64_t o;
+        int32_t n;
+        sort_row_span(ptr, len, stride, list[idx].row, o, n);
+        const int64_t w0 = ws_off[idx];
+        for (int i = tid; i < NW / 4; i += SORTBM_T) ((uint4 *)bits)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        for (int32_t e = tid; e < n; e += SORTBM_T) {
+            const uint32_t c = (uint32_t)col[o + e];
+            atomicOr(&bits[c >> 5], 1u << (c & 31));
+        }
+        __syncthreads();
+        // thread t: words [t * per, (t + 1) * per)
+        int cnt = 0;
+        for (int j = 0; j < per; ++j) {
+            const int wi = tid * per + j;
+            cnt += wi < NW ? __popc(bits[wi]) : 0;
+        }
+        int tot;
+        int run = Team<SORTBM_T>::excl_sum(cnt, tot, scratch);
+        for (int j = 0; j < per; ++j) {
+            const int wi = tid * per + j;
+            if (wi < NW) {
+                if ((wi & 7) == 0) pre8[wi >> 3] = run;
+                run += __popc(bits[wi]);
+            }
+        }
+        __syncthreads();
+        for (int32_t e = tid; e < n; e += SORTBM_T) {
+            const uint32_t c = (uint32_t)col[o + e];
+            const double v = val[o + e];
+            const uint32_t wi = c >> 5;
+            int pos = pre8[wi >> 3] + __popc(bits[wi] & ((1u << (c & 31)) - 1u));
+            for (uint32_t k = wi & ~7u; k < wi; ++k) pos += __popc(bits[k]);
+            wcol[w0 + pos] = (int32_t)c;
+            wval[w0 + pos] = v;
+        }
+        __threadfence_block();
+        __syncthreads();
+        for (int32_t e = tid; e < n; e += SORTBM_T) {
+            col[o + e] = wcol[w0 + e];
+            val[o + e] = wval[w0 + e];
+        }
+        __syncthreads();
+    }
+}
+
 __global__ __launch_bounds__(256) void k_wide_gather(const RowRef *list, int32_t count,
                                                      const int64_t *ws_off, const int64_t *ptr,
                                                      const int32_t *len, int64_t stride,
@@ -1686,7 +1755,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
 
 ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
                               int64_t a_entries, ias_report *rep) {
-    (void)cols;
+    n_cols = cols;
     IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
     const BinSpec ss = sym_spec(), ns = num_spec();
@@ -1744,9 +1813,33 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     bin_starts(c1, st);
     int c;
     IAS_TRY(fork());
-    int lane_no = 0;
+    // Streams by estimated cost, largest first onto the least loaded stream:
+    // pairs of side streams share a hardware queue, so four balanced streams
+    // keep both queues balanced whatever the pairing (round robin left one
+    // queue 1 ms behind the other on K3').  Cost = estimated products x the
+    // kernel's serial ns per product on K3' (short 5, sym3 3.5, sym4 4.2,
+    // sym5 7, bucketed partitions 40: their whole-CU workgroups wait beside
+    // the other bins).
+    int sym_lane[MAX_BINS] = {};
+    {
+        double load[NSIDE] = {};
+        std::vector<std::pair<double, int>> jobs;
+        if (c1.count[sym_part] > 0) jobs.push_back({40.0 * (double)c1.part_prod, sym_part});
+        for (int b = 1; b <= ss.nval; ++b)
+            if (c1.count[b] > 0) {
+                const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
+                const double w = u <= SHORT_MAX ? 5.0 : u <= SYM3_MAX ? 3.5 : u <= SYM4_MAX ? 4.2 : 7.0;
+                jobs.push_back({w * c1.count[b] * 0.5 * (double)(l + u), b});
+            }
+        std::stable_sort(jobs.begin(), jobs.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+        for (const auto &j : jobs) {
+            const int i = (int)(std::min_element(load, load + NSIDE) - load);
+            load[i] += j.first;
+            sym_lane[j.second] = i;
+        }
+    }
     if ((c = c1.count[sym_part]) > 0) {
-        hipStream_t t = (hipStream_t)side_stream(lane_no++);
+        hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
         k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
         k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
@@ -1762,7 +1855,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     }
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
-            hipStream_t t = (hipStream_t)side_stream(lane_no++);
+            hipStream_t t = (hipStream_t)side_stream(sym_lane[b]);
             const int32_t u = SYM2_BINS[b - 1].upper;
             if (u <= SHORT_MAX) {
                 const ShortArgs sh{A, ax, B.col, B.val, SL + st[b], c, nnz, sa.dupn};
@@ -2155,7 +2248,11 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
             if (!radix) (void)hipGetLastError();   // allocation failure: take the bitonic workspace
         }
     }
-    if (nwide > 0 && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
+    // wide rows by the column bitmap when C's columns fit it (the compact
+    // workspace of the radix path, 12 B per entry, is its staging)
+    const bool bitmap_sort = nwide > 0 && !force_global && plan->n_cols > 0 && plan->n_cols <= SORTBM_COLS;
+    if (bitmap_sort && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * slots + 16ull * nwide + 256));
+    if (nwide > 0 && !radix && !bitmap_sort) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     int c;
     if ((c = hc.count[1]) > 0)
         k_sort_lds<32, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
@@ -2169,7 +2266,17 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
         k_sort_lds<1024, 4096, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
     if ((c = hc.count[6]) > 0)
         k_sort_lds<1024, 8192, 1><<<c, 1024, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
-    if ((c = nwide) > 0 && radix) {
+    if ((c = nwide) > 0 && bitmap_sort) {
+        char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
+        double *wv = (double *)b;
+        int32_t *wc = (int32_t *)(wv + slots);
+        const size_t lds = sortbm_lds((int32_t)plan->n_cols);
+        static bool sb_done = false;
+        allow_lds(k_sort_bitmap, sb_done, lds);
+        const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap, SORTBM_T, lds));
+        k_sort_bitmap<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, s>>>(
+            lst(wide), c, coff, ptr, len, stride, col, val, (int32_t)plan->n_cols, wc, wv);
+    } else if ((c = nwide) > 0 && radix) {
         char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
         double *vin = (double *)b;
         double *vout = vin + slots;

@@ -97,8 +97,9 @@ struct ias_plan {
     void *side_stream(int i) const { return (serial || small) ? stream : side[i % NSIDE]; }
     void *host_counters = nullptr;
 
-    // state carried from symbolic() to numeric()
+    // state carried from symbolic() to numeric() (and the row sort)
     int64_t n_rows = 0;
+    int64_t n_cols = 0;      // C's columns
     int64_t n_entries = 0;   // stored entries of A (expanded-A length)
     int64_t nnz_total = 0;
     int64_t flops = 0;
