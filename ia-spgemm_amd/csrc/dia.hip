@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -314,12 +315,25 @@ struct DiaPlan {
     std::vector<int32_t> offc, pst, pja, pkb, maps;
     int32_t lo_a = 0, span_a = 0, lo_b = 0, span_b = 0, lo_c = 0, span_c = 0;
     int64_t flops = 0;                // multiply pairs formed (in range)
+    int device = 0;
     int32_t *d_offc = nullptr, *d_tab = nullptr, *d_maps = nullptr;
     int32_t *d_offa = nullptr, *d_offb = nullptr;
+    // the device tables go back to the block cache, which hands a block out
+    // again only after a device sync (queued kernels of the last call first)
+    ~DiaPlan() {
+        int cur = 0;
+        const bool had = hipGetDevice(&cur) == hipSuccess;
+        for (int32_t *q : {d_offc, d_tab, d_maps, d_offa, d_offb}) dev_free(q, device);
+        if (had) hipSetDevice(cur);   // dev_free selects the plan's device
+    }
 };
+// Plans by key, at most CAP of them: a new key beyond that evicts the least
+// recently used plan (a caller still holding it keeps it alive).
 struct DiaCache {
+    static constexpr size_t CAP = 256;
     std::mutex mu;
-    std::map<std::vector<int64_t>, DiaPlan *> plans;   // never freed: a plan is tiny
+    uint64_t tick = 0;
+    std::map<std::vector<int64_t>, std::pair<std::shared_ptr<const DiaPlan>, uint64_t>> plans;
 };
 DiaCache &dia_cache() {
     static DiaCache *c = new DiaCache;
@@ -331,7 +345,7 @@ ias_status upload_i32(int32_t **d, const std::vector<int32_t> &h, int device) {
     return IAS_SUCCESS;
 }
 ias_status dia_plan_get(const std::vector<int32_t> &offa, const std::vector<int32_t> &offb, int64_t rows,
-                        int64_t a_cols, int64_t b_cols, int device, const DiaPlan **out) {
+                        int64_t a_cols, int64_t b_cols, int device, std::shared_ptr<const DiaPlan> *out) {
     std::vector<int64_t> key{device, rows, a_cols, b_cols, (int64_t)offa.size()};
     key.insert(key.end(), offa.begin(), offa.end());
     key.insert(key.end(), offb.begin(), offb.end());
@@ -339,10 +353,12 @@ ias_status dia_plan_get(const std::vector<int32_t> &offa, const std::vector<int3
     std::lock_guard<std::mutex> g(c.mu);
     auto it = c.plans.find(key);
     if (it != c.plans.end()) {
-        *out = it->second;
+        it->second.second = ++c.tick;
+        *out = it->second.first;
         return IAS_SUCCESS;
     }
-    DiaPlan *P = new DiaPlan;
+    std::shared_ptr<DiaPlan> P = std::make_shared<DiaPlan>();
+    P->device = device;
     const int32_t nda = (int32_t)offa.size(), ndb = (int32_t)offb.size();
     dia_plan(offa.data(), nda, offb.data(), ndb, rows, a_cols, b_cols, P->offc, P->pst, P->pja, P->pkb);
     const int32_t ndc = (int32_t)P->offc.size();
@@ -379,11 +395,15 @@ ias_status dia_plan_get(const std::vector<int32_t> &offa, const std::vector<int3
     if ((st = upload_i32(&P->d_offc, P->offc, device)) || (st = upload_i32(&P->d_tab, tab, device)) ||
         (st = upload_i32(&P->d_maps, P->maps, device)) || (st = upload_i32(&P->d_offa, offa, device)) ||
         (st = upload_i32(&P->d_offb, offb, device))) {
-        for (int32_t *q : {P->d_offc, P->d_tab, P->d_maps, P->d_offa, P->d_offb}) dev_free(q, device);
-        delete P;
-        return st;
+        return st;   // P's destructor frees what was uploaded
     }
-    if (c.plans.size() < 256) c.plans[key] = P;   // beyond that: planned per call (leaked, tiny)
+    if (c.plans.size() >= DiaCache::CAP) {
+        auto lru = c.plans.begin();
+        for (auto j = c.plans.begin(); j != c.plans.end(); ++j)
+            if (j->second.second < lru->second.second) lru = j;
+        c.plans.erase(lru);
+    }
+    c.plans[key] = {P, ++c.tick};
     *out = P;
     return IAS_SUCCESS;
 }
@@ -404,8 +424,11 @@ void dia_events(int device, hipEvent_t *e0, hipEvent_t *e1) {
 }
 }  // namespace
 
-extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
-                                      const ias_opts *opts, ias_report *rep) {
+// into: C is the caller's device DIA (capacity C->num_diagonals diagonals:
+// diagonal_offsets of that many entries, diagonal_ind of rows + cols - 1, val
+// of rows x capacity); C is written in place with num_diagonals = nd_C.
+static ias_status dia_mul(const ias_dia *A, const ias_dia *B, ias_dia *C, const ias_opts *opts,
+                          ias_report *rep, bool into) {
     if (!A || !B || !C) return IAS_ERROR_INVALID_ARGUMENT;
     if (!A->choice || !B->choice) return IAS_ERROR_INFEASIBLE;
     if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
@@ -428,7 +451,7 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     IAS_TRY(read_offsets(A, offa));
     if (B == A) offb = offa;
     else IAS_TRY(read_offsets(B, offb));
-    const DiaPlan *P = nullptr;
+    std::shared_ptr<const DiaPlan> P;
     IAS_TRY(dia_plan_get(offa, offb, A->rows, A->cols, B->cols, device, &P));
     const int32_t ndc = (int32_t)P->offc.size();
 
@@ -482,11 +505,22 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     D.choice = 1;
     D.memory = IAS_MEMORY_DEVICE;
     D.device = device;
-    cl.D = &D;
     const int64_t span = std::max<int64_t>(A->rows + B->cols - 1, 0);
-    IAS_TRY(dev_alloc((void **)&D.diagonal_offsets, 4 * (size_t)ndc, device));
-    IAS_TRY(dev_alloc((void **)&D.diagonal_ind, 4 * (size_t)span, device));
-    IAS_TRY(dev_alloc((void **)&D.val, 8 * (size_t)A->rows * ndc, device));
+    if (into) {
+        if (C->num_diagonals < ndc) {
+            set_last_error("C needs %d diagonals, capacity %d", ndc, C->num_diagonals);
+            C->num_diagonals = ndc;
+            return IAS_ERROR_INSUFFICIENT_CAPACITY;
+        }
+        D.diagonal_offsets = C->diagonal_offsets;
+        D.diagonal_ind = C->diagonal_ind;
+        D.val = C->val;
+    } else {
+        cl.D = &D;
+        IAS_TRY(dev_alloc((void **)&D.diagonal_offsets, 4 * (size_t)ndc, device));
+        IAS_TRY(dev_alloc((void **)&D.diagonal_ind, 4 * (size_t)span, device));
+        IAS_TRY(dev_alloc((void **)&D.val, 8 * (size_t)A->rows * ndc, device));
+    }
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (rep) dia_events(device, &e0, &e1);
@@ -561,7 +595,12 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
         rep->flops = P->flops;
         rep->nnz_c = n;
     }
-    if (out_mem == IAS_MEMORY_HOST) {
+    if (into) {
+        C->rows = D.rows;
+        C->cols = D.cols;
+        C->num_diagonals = ndc;
+        C->choice = 1;
+    } else if (out_mem == IAS_MEMORY_HOST) {
         ias_dia H{};
         IAS_TRY(ias_dia_copy(&D, &H, IAS_MEMORY_HOST, 0));
         *C = H;   // D is freed by the cleanup
@@ -569,5 +608,41 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
         *C = D;
         cl.D = nullptr;
     }
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
+                                      const ias_opts *opts, ias_report *rep) {
+    return dia_mul(A, B, C, opts, rep, false);
+}
+
+extern "C" ias_status ias_dia_mul_dia_into(const ias_dia *A, const ias_dia *B, ias_dia *C,
+                                           const ias_opts *opts, ias_report *rep) {
+    if (!C || C->memory != IAS_MEMORY_DEVICE || C->num_diagonals < 0 || !C->diagonal_ind ||
+        (C->num_diagonals > 0 && (!C->diagonal_offsets || !C->val)))
+        return IAS_ERROR_INVALID_ARGUMENT;
+    ias_opts o;
+    ias_opts_default(&o);
+    if (opts) o = *opts;
+    o.device = C->device;
+    return dia_mul(A, B, C, &o, rep, true);
+}
+
+extern "C" ias_status ias_dia_mul_dia_ndiag(const ias_dia *A, const ias_dia *B, int32_t *nd_c) {
+    if (!A || !B || !nd_c) return IAS_ERROR_INVALID_ARGUMENT;
+    if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
+    std::vector<int32_t> offa(A->num_diagonals), offb(B->num_diagonals);
+    for (auto xo : {std::make_pair(A, &offa), std::make_pair(B, &offb)}) {
+        std::vector<int32_t> &h = *xo.second;
+        if (h.empty()) continue;
+        if (xo.first->memory == IAS_MEMORY_DEVICE)
+            IAS_TRY(dev_copy_d2h(h.data(), xo.first->diagonal_offsets, 4 * h.size(), xo.first->device));
+        else
+            memcpy(h.data(), xo.first->diagonal_offsets, 4 * h.size());
+    }
+    std::vector<int32_t> offc, pst, pja, pkb;
+    dia_plan(offa.data(), (int32_t)offa.size(), offb.data(), (int32_t)offb.size(), A->rows, A->cols, B->cols,
+             offc, pst, pja, pkb);
+    *nd_c = (int32_t)offc.size();
     return IAS_SUCCESS;
 }

@@ -64,10 +64,15 @@ struct BlockCache {
     // (one sync per call that allocates, not one per freed array)
     std::vector<std::pair<void *, size_t>> pending[64];
     size_t held[64] = {};
-    // pending -> free (caller holds the lock and has synchronised the device)
-    void settle(int device) {
-        for (auto &b : pending[device]) free[{device, b.second}].push_back(b.first);
-        pending[device].clear();
+    // pending blocks whose last users were queued before a device sync that
+    // then completed -> free (caller holds the lock; `n` = the size of
+    // pending[device] taken under the lock BEFORE that sync: blocks freed by
+    // another thread after the snapshot may still be in use and stay pending)
+    void settle(int device, size_t n) {
+        auto &p = pending[device];
+        n = std::min(n, p.size());
+        for (size_t i = 0; i < n; ++i) free[{device, p[i].second}].push_back(p[i].first);
+        p.erase(p.begin(), p.begin() + (ptrdiff_t)n);
     }
     static size_t round(size_t b) {
         size_t r = 256;
@@ -75,17 +80,24 @@ struct BlockCache {
         return r;
     }
     // hipFree every cached free block of `device` (caller holds no lock)
-    void trim(int device) {
+    size_t trim(int device) {
         std::vector<void *> drop;
+        size_t bytes = 0;
+        size_t snap;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            snap = pending[device].size();
+        }
         (void)hipDeviceSynchronize();
         {
             std::lock_guard<std::mutex> g(mu);
-            settle(device);
+            settle(device, snap);
             for (auto it = free.begin(); it != free.end();) {
                 if (it->first.first == device) {
                     for (void *q : it->second) {
                         drop.push_back(q);
                         size_of.erase(q);
+                        bytes += it->first.second;
                     }
                     held[device] -= it->first.second * it->second.size();
                     it = free.erase(it);
@@ -95,6 +107,11 @@ struct BlockCache {
             }
         }
         for (void *q : drop) hipFree(q);
+        return bytes;
+    }
+    size_t held_bytes(int device) {
+        std::lock_guard<std::mutex> g(mu);
+        return device >= 0 && device < 64 ? held[device] : 0;
     }
 };
 BlockCache &cache() {
@@ -112,6 +129,7 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
     const size_t want = cached ? BlockCache::round(bytes) : bytes;
     if (cached) {
         bool sync = false;
+        size_t snap = 0;
         {
             std::lock_guard<std::mutex> g(c.mu);
             auto it = c.free.find({device, want});
@@ -122,12 +140,14 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
                 return IAS_SUCCESS;
             }
             for (auto &b : c.pending[device]) sync = sync || b.second == want;
+            snap = c.pending[device].size();
         }
         if (sync) {
-            // a freed block of this size exists: wait for its last users
+            // a freed block of this size exists: wait for its last users (only
+            // the blocks pending before this sync are settled by it)
             HIPC(hipDeviceSynchronize());
             std::lock_guard<std::mutex> g(c.mu);
-            c.settle(device);
+            c.settle(device, snap);
             auto it = c.free.find({device, want});
             if (it != c.free.end() && !it->second.empty()) {
                 *p = it->second.back();
@@ -140,7 +160,7 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
     hipError_t e = hipMalloc(p, want);
     if (e == hipErrorOutOfMemory && device >= 0 && device < 64) {
         (void)hipGetLastError();
-        c.trim(device);
+        release_device_memory(device, nullptr);
         e = hipMalloc(p, want);
     }
     HIPC(e);
@@ -469,6 +489,19 @@ DefaultPlans &default_plans() {
     static DefaultPlans *d = new DefaultPlans;   // never destroyed (plans may be in use at exit)
     return *d;
 }
+}  // namespace
+
+size_t ias::release_device_memory(int device, const ias_plan *keep) {
+    size_t bytes = cache().trim(device);
+    DefaultPlans &d = default_plans();
+    std::lock_guard<std::mutex> g(d.mu);
+    auto it = d.plan.find(device);
+    if (it != d.plan.end() && it->second && it->second != keep && !d.busy[device])
+        bytes += it->second->release_workspace();
+    return bytes;
+}
+
+namespace {
 bool default_plan_on() {
     static const bool on = [] {
         const char *e = getenv("IAS_DEFAULT_PLAN");
@@ -794,6 +827,29 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
     } else {
         *C = D;
     }
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_device_release(int32_t device, int64_t *released) {
+    int32_t n = 0;
+    IAS_TRY(ias_device_count(&n));
+    if (device < 0 || device >= n) return IAS_ERROR_INVALID_ARGUMENT;
+    HIPC(hipSetDevice(device));
+    const size_t b = release_device_memory(device, nullptr);
+    if (released) *released = (int64_t)b;
+    return IAS_SUCCESS;
+}
+
+extern "C" ias_status ias_device_cached_bytes(int32_t device, int64_t *bytes) {
+    if (!bytes) return IAS_ERROR_INVALID_ARGUMENT;
+    size_t b = cache().held_bytes(device);
+    DefaultPlans &d = default_plans();
+    {
+        std::lock_guard<std::mutex> g(d.mu);
+        auto it = d.plan.find(device);
+        if (it != d.plan.end() && it->second) b += it->second->workspace_bytes();
+    }
+    *bytes = (int64_t)b;
     return IAS_SUCCESS;
 }
 

@@ -21,6 +21,10 @@ ias_status dev_free(void *p, int device);
 ias_status dev_copy_h2d(void *dst, const void *src, size_t bytes, int device);
 ias_status dev_copy_d2h(void *dst, const void *src, size_t bytes, int device);
 ias_status dev_memset(void *p, int value, size_t bytes, int device);
+// Out-of-memory relief: hipFree the device's cached free blocks and the
+// workspace of its idle default plan (never `keep`, the plan of the caller);
+// returns the bytes released.
+size_t release_device_memory(int device, const ias_plan *keep);
 
 // Record the last HIP/internal error message for ias_status_string's detail.
 void set_last_error(const char *fmt, ...);

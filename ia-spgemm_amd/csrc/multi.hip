@@ -428,9 +428,14 @@ extern "C" ias_status ias_dist_allgatherv_csr(ias_dist *d, const ias_csr *Cl, ia
     HIPC(hipSetDevice(d->device));
     hipStream_t s = (hipStream_t)stream;
     const int P = d->nranks;
-    // C_local may be a row view: its entries start at row_ptr[0]
+    // C_local may be a row view: its entries start at row_ptr[0].  Read on the
+    // caller's stream after the work it queued (a non-blocking stream may
+    // still be producing C_local).
     int64_t rp0 = 0;
-    if (Cl->rows > 0) IAS_TRY(dev_copy_d2h(&rp0, Cl->row_ptr, sizeof(int64_t), d->device));
+    if (Cl->rows > 0) {
+        HIPC(hipMemcpyAsync(&rp0, Cl->row_ptr, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        HIPC(hipStreamSynchronize(s));
+    }
     // per-rank (rows, nnz)
     std::vector<int64_t> h(2 * (P + 1));
     {

@@ -137,8 +137,9 @@ __device__ __forceinline__ int32_t short_gather(const ShortArgs &a, ShortLds<K, 
 __device__ __forceinline__ uint32_t sh_hash(int32_t c, int lg) { return ((uint32_t)c * 0x9E3779B1u) >> (32 - lg); }
 
 // Insert the K columns; slot[k] = the column's slot, made = new columns.  The
-// first probe of all K items is issued back to back (items beyond P CAS the
-// empty key into its own home slot: a no-op); collisions then probe on.
+// first probe of all K items is issued back to back (items beyond P issue
+// none: their CAS of the empty key into its home slot, one address for every
+// idle lane, serialised in one bank); collisions then probe on.
 template <int S, int K>
 __device__ __forceinline__ int sh_insert(int32_t *keys, const int32_t (&c)[K], uint32_t (&slot)[K]) {
     constexpr int LG = __builtin_ctz(S);
@@ -147,7 +148,9 @@ __device__ __forceinline__ int sh_insert(int32_t *keys, const int32_t (&c)[K], u
 #pragma unroll
     for (int k = 0; k < K; ++k) {
         slot[k] = sh_hash(c[k], LG);
-        g[k] = atomicCAS(&keys[slot[k]], SH_EMPTY, c[k]);
+        int32_t o = SH_EMPTY;
+        if (c[k] != SH_EMPTY) o = atomicCAS(&keys[slot[k]], SH_EMPTY, c[k]);
+        g[k] = o;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -275,7 +278,9 @@ __device__ __forceinline__ void sh_insert_r(T (&L)[R], const int32_t (&c)[R][K],
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             slot[r][k] = sh_hash(c[r][k], LG);
-            g[r][k] = atomicCAS(&L[r].keys[slot[r][k]], SH_EMPTY, c[r][k]);
+            int32_t o = SH_EMPTY;   // items beyond P issue nothing (see sh_insert)
+            if (c[r][k] != SH_EMPTY) o = atomicCAS(&L[r].keys[slot[r][k]], SH_EMPTY, c[r][k]);
+            g[r][k] = o;
         }
 #pragma unroll
     for (int r = 0; r < R; ++r) {

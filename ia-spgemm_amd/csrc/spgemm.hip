@@ -1614,9 +1614,40 @@ ias_status ias_plan::reserve(void **buf, size_t *cap, size_t bytes) {
     *buf = nullptr;
     *cap = 0;
     const size_t want = std::max<size_t>(bytes + bytes / 8, 256);
-    HIPC(hipMalloc(buf, want));
+    hipError_t e = hipMalloc(buf, want);
+    if (e == hipErrorOutOfMemory) {
+        // the block cache and an idle default plan may hold what is missing
+        (void)hipGetLastError();
+        release_device_memory(device, this);
+        e = hipMalloc(buf, want);
+    }
+    if (e != hipSuccess) *buf = nullptr;
+    HIPC(e);
     *cap = want;
     return IAS_SUCCESS;
+}
+
+size_t ias_plan::release_workspace() {
+    hipSetDevice(device);
+    if (stream) hipStreamSynchronize((hipStream_t)stream);
+    for (int i = 0; i < NSIDE; ++i)
+        if (side[i]) hipStreamSynchronize((hipStream_t)side[i]);
+    size_t b = 0;
+    for (auto &x : bufs) {
+        if (x.p) {
+            hipFree(x.p);
+            b += x.cap;
+        }
+        x = Buf{};
+    }
+    last_a = last_b = nullptr;   // a compute() after this needs a new nnz()
+    return b;
+}
+
+size_t ias_plan::workspace_bytes() const {
+    size_t b = 0;
+    for (const auto &x : bufs) b += x.p ? x.cap : 0;
+    return b;
 }
 
 ias_plan::~ias_plan() {

@@ -121,6 +121,10 @@ struct ias_plan {
     ias_status init(int device, void *stream);
     ias_status reserve(void **buf, size_t *cap, size_t bytes);
     ias_status reserve(int which, size_t bytes) { return reserve(&bufs[which].p, &bufs[which].cap, bytes); }
+    // hipFree every workspace buffer once the plan's streams are idle (they
+    // grow again on the next call); returns the bytes freed
+    size_t release_workspace();
+    size_t workspace_bytes() const;
     // a_entries: stored entries of A (CSR: nnz of the view; ELL: rows * width)
     ias_status analysis_launch(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                                int64_t a_entries);

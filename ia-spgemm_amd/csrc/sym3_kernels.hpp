@@ -273,7 +273,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
                 const bool in = k0 + t < nwin;
                 const uint32_t h = s3_h1(cc, LDS::F1B);
                 bit[t] = in ? 1u << (h & 31) : 0u;
-                old[t] = atomicOr(&L.f1[in ? h >> 5 : 0u], bit[t]);
+                // lanes past the row issue nothing (a same-address atomic of
+                // every idle lane serialises in one bank)
+                uint32_t o = 0u;
+                if (in) o = atomicOr(&L.f1[h >> 5], bit[t]);
+                old[t] = o;
             }
 #pragma unroll
             for (int t = 0; t < CH; ++t) {

@@ -167,7 +167,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
                 const bool in = 64 * (k0 + t) + lane < P;
                 const uint32_t h = s3_h1(c[t], LDS::F1B);
                 bit[t] = in ? 1u << (h & 31) : 0u;
-                old[t] = atomicOr(&L.f1[in ? h >> 5 : 0u], bit[t]);
+                uint32_t o = 0u;   // lanes / windows past the row issue nothing
+                if (in) o = atomicOr(&L.f1[h >> 5], bit[t]);
+                old[t] = o;
             }
 #pragma unroll
             for (int t = 0; t < KC; ++t) {

@@ -102,6 +102,7 @@ EXPORTS = [
     "ias_dia_to_csr", "ias_csr_transpose",
     "ias_sizeof_csr", "ias_sizeof_coo", "ias_sizeof_ell", "ias_sizeof_dia",
     "ias_csr_mul_csr", "ias_coo_mul_coo", "ias_ell_mul_ell", "ias_dia_mul_dia",
+    "ias_dia_mul_dia_into", "ias_dia_mul_dia_ndiag", "ias_device_release", "ias_device_cached_bytes",
     "ias_csr_mul_csr_nnz", "ias_csr_mul_csr_compute", "ias_csr_mul_csr_into",
     "ias_flops", "ias_sum_csr", "ias_sum_coo", "ias_sum_ell", "ias_sum_dia",
     "ias_csr_row_view", "ias_partition_rows", "ias_row_ptr_shift",
@@ -155,6 +156,10 @@ def _load():
         "ias_coo_mul_coo": (C.c_int, [P(Coo), P(Coo), P(Coo), P(Opts), P(Report)]),
         "ias_ell_mul_ell": (C.c_int, [P(Ell), P(Ell), P(Ell), P(Opts), P(Report)]),
         "ias_dia_mul_dia": (C.c_int, [P(Dia), P(Dia), P(Dia), P(Opts), P(Report)]),
+        "ias_dia_mul_dia_into": (C.c_int, [P(Dia), P(Dia), P(Dia), P(Opts), P(Report)]),
+        "ias_dia_mul_dia_ndiag": (C.c_int, [P(Dia), P(Dia), i32p]),
+        "ias_device_release": (C.c_int, [C.c_int32, i64p]),
+        "ias_device_cached_bytes": (C.c_int, [C.c_int32, i64p]),
         "ias_csr_mul_csr_nnz": (C.c_int, [C.c_void_p, P(Csr), P(Csr), i64p, i64p, P(Report)]),
         "ias_csr_mul_csr_compute": (C.c_int, [C.c_void_p, P(Csr), P(Csr), P(Csr), C.c_int32, P(Report)]),
         "ias_csr_mul_csr_into": (C.c_int, [C.c_void_p, P(Csr), P(Csr), P(Csr), C.c_int32, P(Report)]),

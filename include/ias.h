@@ -172,6 +172,16 @@ void        ias_opts_default(ias_opts *opts);
  * creates per call (GPU/detail/cusparse/common_cusparse.h:44-72). */
 ias_status ias_plan_create(ias_plan **plan, int32_t device, void *stream);
 ias_status ias_plan_destroy(ias_plan *plan);
+/* Memory the library keeps on a device between calls: the block cache of
+ * freed output blocks and the workspace of the per-device default plan (the
+ * plan of calls made without one).  Both are released by themselves when a
+ * device allocation of the library runs out of memory; a caller about to
+ * allocate a lot of its own can release them first.  (No reference
+ * counterpart: the reference creates a cuSPARSE handle per call,
+ * GPU/detail/cusparse/common_cusparse.h:44, and keeps nothing between
+ * calls.)  released_bytes may be NULL. */
+ias_status ias_device_release(int32_t device, int64_t *released_bytes);
+ias_status ias_device_cached_bytes(int32_t device, int64_t *bytes);
 
 /* ---------------------------------------------------------------- memory */
 ias_status ias_csr_alloc(ias_csr *m, int64_t rows, int64_t cols, int64_t nnz,
@@ -243,6 +253,18 @@ ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_ell *C,
  * environment forces either kernel. */
 ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
                            const ias_opts *opts, ias_report *report);  /* DIA_mul_DIA dia:101-195 */
+/* The same into caller-provided device arrays (no allocation in the call; the
+ * reference's GPU DIA path, GPU/detail/dia_dev/common_dia_dev.h:85-122, writes
+ * into C arrays allocated before its kernels): C->memory = device, C->device
+ * the compute device, C->num_diagonals = the capacity in diagonals,
+ * diagonal_offsets >= capacity entries, diagonal_ind >= rows + cols - 1, val >=
+ * rows x capacity.  On success C->num_diagonals = nd_C and val is rows x nd_C
+ * row-major; a capacity below nd_C returns IAS_ERROR_INSUFFICIENT_CAPACITY with
+ * C->num_diagonals = nd_C.  ias_dia_mul_dia_ndiag gives nd_C from the offsets
+ * alone (dia:107-140's reachability rule). */
+ias_status ias_dia_mul_dia_into(const ias_dia *A, const ias_dia *B, ias_dia *C,
+                                const ias_opts *opts, ias_report *report);
+ias_status ias_dia_mul_dia_ndiag(const ias_dia *A, const ias_dia *B, int32_t *nd_c);
 
 /* Two-phase form on device-resident CSR, the split the reference's GPU path
  * uses (cusparseXcsrgemmNnz + cusparseDcsrgemm, GPU/detail/cusparse/
