@@ -74,7 +74,7 @@ def parse(argv=None):
                         "(rehearses one rank of the multi-GPU run on one GPU; reports per-rank numbers); "
                         "'R1,R2,...' or 'all' run several shards one after the other, one line each")
     p.add_argument("--format", default="csr", choices=["csr", "dia"],
-                   help="dia: C = A*A through the DIA kernel (ias_dia_mul_dia) on device-resident DIA "
+                   help="dia: C = A*A through the DIA kernel (ias_dia_mul_dia_into) on device-resident DIA "
                         "operands (banded configs, N=1)")
     p.add_argument("--no-gather", action="store_true", help="N>1: skip the allgatherv measurement")
     p.add_argument("--gather-reps", type=int, default=1, help="N>1: repetitions of the allgatherv measurement")
@@ -282,7 +282,7 @@ def main(argv=None):
         ms_flat = statistics.mean(x[4] for x in reps)
         flat_bytes = 12 * int(rep.stream_nnz) + bytes_a + bytes_b
         gather_bytes = 12 * int(rep.stream_products)
-        kname = "k_numeric_flat" if os.environ.get("IAS_NUM2", "1") == "0" else "k_num2"
+        kname = "k_num2"
         units = {"products": int(rep.stream_products), "c_entries": int(rep.stream_nnz)}
         # the pass is 1 to 3 launches (rows by duplicate class; each class's
         # fix-ups overlap the rest): ms_stream sums the launches' own durations
@@ -393,10 +393,12 @@ def main(argv=None):
             if rank == 0:
                 out["same_matrix_1gpu"] = anchor
         if rank == 0 and world == 1 and as_ranks is None and not args.no_one_shot:
+            # C's buffers go back to torch's cache, not to the driver: the
+            # one-shot call then allocates fresh memory beside them, as a caller
+            # holding its own tensors would
             del cbufs, step
             step = cbufs = None
-            torch.cuda.empty_cache()
-            out["one_shot"] = one_shot(dcsr(0, rows, rp, nnz_a), local, out["ms_per_step"])
+            out["one_shot"] = one_shot(dcsr(0, rows, rp, nnz_a), local, out["ms_per_step"], nnz_c_step=out["config"]["nnz_c"])
         if rank == 0 and world == 1 and as_ranks is None and not args.no_cpu_baseline and \
                 kind in ("rmat", "band", "ell"):
             out["cpu_baseline"] = cpu_baseline(A, flops_total, args.cpu_threads, args.cpu_full)
@@ -486,14 +488,28 @@ def same_matrix_1gpu(plan, Afull, Bm, rows, cols, local, dev, rank, ms_dist, flo
     return res
 
 
-def one_shot(Am, local, ms_step):
+def one_shot(Am, local, ms_step, nnz_c_step=0):
     """Two ias_csr_mul_csr calls with device-resident A = B and a device C the
     library allocates (no plan, no stream passed: the per-device default plan),
     as the reference's cuSPARSE timed region includes C's allocation
     (GPU/detail/cusparse/common_cusparse.h:74-93): wall and device ms of the
-    first call (workspace allocation included) and of the second."""
+    first call (workspace allocation included) and of the second.  Before them,
+    `alloc_probe_ms`: one hipMalloc + hipFree of C's size (through
+    ias_csr_alloc, blocks this large bypass the block cache) — what fresh
+    device memory costs on this box, the part of the first call no kernel
+    change can remove."""
     import ias
     res = {}
+    if nnz_c_step > 0:
+        m = ias.Csr()
+        t = time.perf_counter()
+        ias.check(ias.lib.ias_csr_alloc(C.byref(m), Am.rows, Am.cols, nnz_c_step, ias.MEMORY_DEVICE, local),
+                  "alloc probe")
+        ta = time.perf_counter()
+        ias.lib.ias_csr_free(C.byref(m))
+        tf = time.perf_counter()
+        res["alloc_probe_ms"] = {"bytes": 12 * nnz_c_step + 8 * (Am.rows + 1),
+                                 "alloc": round(1e3 * (ta - t), 3), "free": round(1e3 * (tf - ta), 3)}
     for tag in ("first", "second"):
         c, rep = ias.Csr(), ias.Report()
         o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=local)
@@ -510,9 +526,12 @@ def one_shot(Am, local, ms_step):
 
 
 def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
-    """One step = ias_dia_mul_dia(A, A) on device-resident DIA operands (C
-    allocated by the library on the device and freed after the step, as the
-    ABI hands it over); the kernel time is the call's event-timed ms_total."""
+    """One step = ias_dia_mul_dia_into(A, A, C) on device-resident DIA operands
+    into a device C allocated once before the loop (the reference's GPU DIA
+    path writes into C arrays allocated before its kernels,
+    GPU/detail/dia_dev/common_dia_dev.h:85-122); the kernel time is the call's
+    event-timed ms_total.  The library-allocating ias_dia_mul_dia (C allocated
+    and freed every call) is timed after the loop as `alloc_call`."""
     import torch
     import ias
     s = A.struct()
@@ -525,12 +544,30 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
     ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
     o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=local, plan=plan)
     rep = ias.Report()
-    ndc = [0]
+    nd = C.c_int32(0)
+    ias.check(ias.lib.ias_dia_mul_dia_ndiag(C.byref(da), C.byref(da), C.byref(nd)), "ndiag")
+    ndc = [int(nd.value)]
+    rows_a, cols_b = int(da.rows), int(da.cols)
+    dev = torch.device("cuda", local)
+    c_off = torch.empty(max(ndc[0], 1), dtype=torch.int32, device=dev)
+    c_ind = torch.empty(max(rows_a + cols_b - 1, 1), dtype=torch.int32, device=dev)
+    c_val = torch.empty(max(rows_a * ndc[0], 1), dtype=torch.float64, device=dev)
+
+    def cdia():
+        return ias.Dia(rows=rows_a, cols=cols_b, num_diagonals=ndc[0], choice=1,
+                       diagonal_offsets=C.cast(C.c_void_p(c_off.data_ptr()), ias.i32p),
+                       diagonal_ind=C.cast(C.c_void_p(c_ind.data_ptr()), ias.i32p),
+                       val=C.cast(C.c_void_p(c_val.data_ptr()), ias.f64p), memory=ias.MEMORY_DEVICE, device=local)
+    Cd = cdia()
 
     def step():
+        Cd.num_diagonals = ndc[0]
+        ias.check(ias.lib.ias_dia_mul_dia_into(C.byref(da), C.byref(da), C.byref(Cd), C.byref(o), C.byref(rep)),
+                  "dia into")
+
+    def step_alloc():
         dc = ias.Dia()
         ias.check(ias.lib.ias_dia_mul_dia(C.byref(da), C.byref(da), C.byref(dc), C.byref(o), C.byref(rep)), "dia")
-        ndc[0] = int(dc.num_diagonals)
         ias.lib.ias_dia_free(C.byref(dc))
 
     for _ in range(args.warmup):
@@ -544,6 +581,13 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
     torch.cuda.synchronize()
     ms_step = 1e3 * (time.perf_counter() - t0) / args.steps
     ms_k = statistics.mean(kms)
+    step_alloc()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step_alloc()
+    torch.cuda.synchronize()
+    ms_alloc = 1e3 * (time.perf_counter() - t1) / args.steps
     rows = int(A.rows)
     alg = 8 * rows * (2 * nda + ndc[0]) + 4 * (2 * nda + ndc[0])   # A, B (= A) read, C written
     kname = {1: "k_dia_tile", 2: "k_dia_mfma", 3: "k_dia_mul"}.get(int(rep.kernel), "?")   # the library's choice
@@ -566,6 +610,8 @@ def run_dia(args, A, kind, prm, desc, flops_total, local, t_gen):
             "alg_bytes_formula": "8*rows*(nd_A + nd_B + nd_C) + 4*(nd_A + nd_B + nd_C)",
             "ms_per_launch": round(ms_k, 4),
         },
+        "alloc_call": {"what": "ias_dia_mul_dia (library-allocated device C, freed every call), same loop",
+                       "ms_per_step": round(ms_alloc, 4)},
         "setup_s": round(t_gen, 2),
     }
     if not args.no_cpu_baseline:

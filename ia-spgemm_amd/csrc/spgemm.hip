@@ -159,49 +159,64 @@ __device__ __forceinline__ void count_bins(const BinSpec &sp, const int (&b)[R],
 // difference of the product offsets, the symbolic bin counts, total flops
 // and the max products per row.
 constexpr int AN_BLOCK = 256;
-constexpr int AN_U = 4;   // entries per thread in flight
+constexpr int AN_U = 8;   // entries per thread: a block is one scan tile (SCAN_TILE = AN_BLOCK * AN_U)
 
 // Expanded A, flat over entries (ELL, A.ptr null: padding entries beyond
-// len[row] get no products).
-__global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t a_entries, AxOut ax) {
+// len[row] get no products); each block also writes its tile's sum of B-row
+// lengths into `partial` — the reduce step of the product-offset scan
+// (k_scan_partials + k_scan_apply finish it), so the lengths are not read back.
+__global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t a_entries, AxOut ax,
+                                                         int64_t *partial) {
     const int64_t abase = A.base();
-    const int64_t step = (int64_t)gridDim.x * AN_BLOCK * AN_U;
-    for (int64_t q0 = (int64_t)blockIdx.x * AN_BLOCK * AN_U + threadIdx.x; q0 < a_entries; q0 += step) {
-        int32_t j[AN_U], bn[AN_U];
-        int64_t bs[AN_U];
-        double av[AN_U];
-        bool ok[AN_U];
+    const int64_t q0 = (int64_t)blockIdx.x * AN_BLOCK * AN_U + threadIdx.x;
+    int32_t j[AN_U], bn[AN_U];
+    int64_t bs[AN_U];
+    double av[AN_U];
+    bool ok[AN_U];
 #pragma unroll
-        for (int u = 0; u < AN_U; ++u) {
-            const int64_t q = q0 + (int64_t)u * AN_BLOCK;
-            ok[u] = q < a_entries;
-            if (ok[u] && !A.ptr) ok[u] = (q % A.stride) < A.len[q / A.stride];
-            j[u] = ok[u] ? A.col[abase + q] : 0;
-        }
+    for (int u = 0; u < AN_U; ++u) {
+        const int64_t q = q0 + (int64_t)u * AN_BLOCK;
+        ok[u] = q < a_entries;
+        if (ok[u] && !A.ptr) ok[u] = (q % A.stride) < A.len[q / A.stride];
+        j[u] = ok[u] ? A.col[abase + q] : 0;
+    }
+    int64_t sum = 0;
 #pragma unroll
-        for (int u = 0; u < AN_U; ++u) {   // all loads before any store (no alias ordering)
-            bn[u] = 0;
-            bs[u] = 0;
-            av[u] = 0.0;
-            if (ok[u]) {
-                B.row(j[u], bs[u], bn[u]);
-                if (ax.aval) av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
-            }
+    for (int u = 0; u < AN_U; ++u) {   // all loads before any store (no alias ordering)
+        bn[u] = 0;
+        bs[u] = 0;
+        av[u] = 0.0;
+        if (ok[u]) {
+            B.row(j[u], bs[u], bn[u]);
+            if (ax.aval) av[u] = A.val[abase + q0 + (int64_t)u * AN_BLOCK];
         }
-        if (ax.wide_b) {
-            bool wide = false;
+        sum += bn[u];
+    }
+    if (ax.wide_b) {
+        bool wide = false;
 #pragma unroll
-            for (int u = 0; u < AN_U; ++u) wide |= bs[u] + bn[u] > (1ll << 30);
-            if (wide) *ax.wide_b = 1;
-        }
+        for (int u = 0; u < AN_U; ++u) wide |= bs[u] + bn[u] > (1ll << 30);
+        if (wide) *ax.wide_b = 1;
+    }
 #pragma unroll
-        for (int u = 0; u < AN_U; ++u) {
-            const int64_t q = q0 + (int64_t)u * AN_BLOCK;
-            if (q >= a_entries) continue;
-            ax.bstart[q] = bs[u];
-            ax.blen[q] = bn[u];
-            if (ax.aval) ax.aval[q] = av[u];
-        }
+    for (int u = 0; u < AN_U; ++u) {
+        const int64_t q = q0 + (int64_t)u * AN_BLOCK;
+        if (q >= a_entries) continue;
+        ax.bstart[q] = bs[u];
+        ax.blen[q] = bn[u];
+        if (ax.aval) ax.aval[q] = av[u];
+    }
+    // the tile's sum
+#pragma unroll
+    for (int d = WAVE / 2; d > 0; d >>= 1) sum += __shfl_down(sum, d);
+    __shared__ int64_t ws[AN_BLOCK / WAVE];
+    if ((threadIdx.x & (WAVE - 1)) == 0) ws[threadIdx.x / WAVE] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+#pragma unroll
+        for (int i = 0; i < AN_BLOCK / WAVE; ++i) t += ws[i];
+        partial[blockIdx.x] = t;
     }
 }
 
@@ -473,10 +488,12 @@ __global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(Rows A, AxView ax, con
                                                           const int64_t *poff, const int32_t *bcol,
                                                           const RowRef *list, int32_t count,
                                                           const int64_t *pfirst, const int64_t *pboff,
-                                                          int32_t part_cap, uint2 *bucket, PartSpan *spans) {
+                                                          int32_t part_cap, uint2 *bucket, PartSpan *spans,
+                                                          const int32_t *pdone) {
     __shared__ uint32_t cnt[PB_MAXP];
     __shared__ int scratch[32];
     const RowRef ref = list[blockIdx.x];
+    if (pdone && pdone[ref.row]) return;   // resolved by k_sym5<..., PART>
     const uint32_t np = nparts_of(ref.n, part_cap);
     const int64_t it0 = pfirst[ref.row];
     const int tid = threadIdx.x;
@@ -571,13 +588,15 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
                                                         Bitmap bm, int32_t *nnz_row, uint2 *gpairs,
                                                         const int64_t *dup_off, int32_t *dupn,
                                                         int32_t div, int32_t dmax, int *overflow,
-                                                        const uint2 *bucket, const PartSpan *spans) {
+                                                        const uint2 *bucket, const PartSpan *spans,
+                                                        const int32_t *pdone) {
     __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
     __shared__ __attribute__((aligned(16))) uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
     const PartItem it = items[blockIdx.x];
     const int64_t row = it.ref.row;
+    if (pdone && pdone[row]) return;
     Timer tmr;
     tmr.start();
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
@@ -603,9 +622,10 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
 
 // Exclusive popcount prefix of each partitioned row's first-touch bitmap.
 __global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32_t count,
-                                                       const int32_t *prod, Bitmap bm) {
+                                                       const int32_t *prod, Bitmap bm, const int32_t *pdone) {
     __shared__ int scratch[8];
     const int64_t row = list[blockIdx.x].row;
+    if (pdone && pdone[row]) return;
     const int64_t W = (prod[row] + 31) / 32;
     const uint32_t *bits = bm.bits + bm.off[row];
     uint32_t *pref = bm.pref + bm.off[row];
@@ -626,9 +646,10 @@ __global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32
 __global__ __launch_bounds__(256) void k_dup_place(const RowRef *list, int32_t count, Bitmap bm,
                                                    const uint2 *gpairs, const int64_t *dup_off,
                                                    int32_t *dupn, int32_t *gdupt, int32_t div,
-                                                   int32_t dmax) {
+                                                   int32_t dmax, const int32_t *pdone) {
     const RowRef ref = list[blockIdx.x];
     const int64_t row = ref.row;
+    if (pdone && pdone[row]) return;
     const int32_t cnt = dupn[row];
     const int32_t cap = div > 0 ? min(ref.n / div, dmax) : 0;
     if (cnt > cap) {
@@ -859,6 +880,7 @@ __global__ __launch_bounds__(TEAM) void k_numeric_global(AxView ax, Rows B, cons
 constexpr int SCAN_BLOCK = 256;
 constexpr int SCAN_ITEMS = 8;
 constexpr int SCAN_TILE = SCAN_BLOCK * SCAN_ITEMS;
+static_assert(SCAN_TILE == AN_BLOCK * AN_U, "k_an_entries blocks are scan tiles");
 
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const int32_t *in, int64_t n,
                                                             int64_t *partial, int32_t *max_out) {
@@ -969,11 +991,11 @@ __global__ void k_fill_rows(const int64_t *ptr, int64_t rows, int32_t *row_idx) 
 }
 
 // ---------------------------------------------------------------- row sort
-// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (2048 by default,
-// IAS_SORT_WIDE_MIN moves it, up to 8192) get a bitonic sort of (col, val) in
-// LDS; the LDS bins above 2048 entries (4096 / 8192) only run when the knob is
-// raised.  Longer rows go through one segmented radix sort over a compact
-// workspace (k_wide_gather), or, when that workspace cannot be had (or
+// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (8192 by default,
+// IAS_SORT_WIDE_MIN lowers it) get a bucket sort in LDS (k_sort_bucket).
+// Longer rows: the column bitmap sort (k_sort_bitmap) when C has at most 2^20
+// columns, else one segmented radix sort over a compact workspace
+// (k_wide_gather), or, when that workspace cannot be had (or
 // IAS_SORT_GLOBAL=1), a bitonic sort per row in a global workspace
 // (k_sort_global).  Columns of a row are distinct, so the order is unique.
 template <int TEAM>
@@ -1011,37 +1033,120 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
     }
 }
 
-template <int TEAM, int CAP, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_sort_lds(const RowRef *list, int32_t count,
-                                                         const int64_t *ptr, const int32_t *len,
-                                                         int64_t stride, int32_t *col, double *val) {
+// Rows of up to TEAM * E entries sorted by a bucket pass in LDS: the row's
+// columns are distinct, so an entry's sorted position is the number of the
+// row's columns below it.  Buckets split the row's column range [min, max]
+// into nb ~ n/4 equal parts (a monotone map, so bucket order is key order);
+// an entry's position = its bucket's start (a scan of the bucket counts) +
+// the keys of its bucket below it (a short loop over the bucket's keys,
+// which are ~4 on average: O(n) work per row, values never leave registers).
+// One read and one write of each entry, three or four team barriers per row
+// (the bitonic sort it replaces needed one per stage, log2(n)^2 / 2 of them).
+template <int TEAM, int E, int TPW>
+__global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
+                                                           const int64_t *ptr, const int32_t *len,
+                                                           int64_t stride, int32_t *col, double *val) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    using TM = Team<TEAM>;
+    constexpr int CAP = TEAM * E;
+    constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
+    constexpr int NBT = (NBM + TEAM - 1) / TEAM;      // bucket counts per thread in the scan
     __shared__ int32_t sk[TPW][CAP];
-    __shared__ double sv[TPW][CAP];
+    __shared__ uint32_t hist[TPW][NBM + 1];
+    __shared__ int scratch[TPW][64];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    const int lane = Team<TEAM>::lane();
+    const int lane = TM::lane();
     const int64_t idx = (int64_t)blockIdx.x * TPW + team;
     const int64_t row = idx < count ? list[idx].row : -1;
     int64_t o = 0;
     int32_t n = 0;
     if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
-    // A workgroup-sized team sorts only the next power of two above its row
-    // (the bins are 4x wide, so a fixed CAP sorted up to 4x the row); teams
-    // sharing a wave keep CAP so their loop trips stay uniform.
-    uint32_t cap = CAP;
-    if constexpr (TPW == 1) {
-        cap = 2;
-        while (cap < (uint32_t)n) cap <<= 1;
+    int32_t c[E];
+    double v[E];
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        c[k] = 0;
+        v[k] = 0.0;
+        if (e < n) {
+            c[k] = col[o + e];
+            v[k] = val[o + e];
+            lo = min(lo, c[k]);
+            hi = max(hi, c[k]);
+        }
     }
-    for (uint32_t e = lane; e < cap; e += TEAM) {
-        sk[team][e] = e < (uint32_t)n ? col[o + e] : INT32_MAX;
-        sv[team][e] = e < (uint32_t)n ? val[o + e] : 0.0;
+    // the row's column range (team min / max)
+    {
+        constexpr int W = TEAM < WAVE ? TEAM : WAVE;
+#pragma unroll
+        for (int d = W / 2; d > 0; d >>= 1) {
+            lo = min(lo, __shfl_xor(lo, d, W));
+            hi = max(hi, __shfl_xor(hi, d, W));
+        }
+        if constexpr (TM::MULTI) {
+            const int w = lane / WAVE;
+            if ((lane & (WAVE - 1)) == 0) {
+                scratch[0][2 * w] = lo;
+                scratch[0][2 * w + 1] = hi;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < TM::NWAVES; ++i) {
+                lo = min(lo, scratch[0][2 * i]);
+                hi = max(hi, scratch[0][2 * i + 1]);
+            }
+        }
     }
-    Team<TEAM>::sync();
-    bitonic<TEAM>(sk[team], sv[team], cap);
-    for (int e = lane; e < n; e += TEAM) {
-        col[o + e] = sk[team][e];
-        val[o + e] = sv[team][e];
+    // nb: a power of two near n / 4 (at least 1, at most NBM)
+    int nb = 1;
+    while (nb < NBM && 4 * nb * 2 <= n) nb <<= 1;
+    for (int i = lane; i <= nb; i += TEAM) hist[team][i] = 0u;
+    TM::sync();   // (multi-wave: also every wave's min / max read before scratch is reused)
+    const float scale = n > 0 ? (float)nb / ((float)((uint32_t)(hi - lo)) + 1.0f) : 0.0f;
+    int b[E];
+    uint32_t pib[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        b[k] = min((int)((float)((uint32_t)(c[k] - lo)) * scale), nb - 1);
+        pib[k] = 0u;
+        if (e < n) pib[k] = atomicAdd(&hist[team][b[k]], 1u);
+    }
+    TM::sync();
+    // bucket starts: exclusive scan of the counts (NBT per thread, in order)
+    {
+        uint32_t cnt[NBT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < NBT; ++j) {
+            const int i = lane * NBT + j;
+            cnt[j] = i < nb ? hist[team][i] : 0u;
+            sum += cnt[j];
+        }
+        int tot;
+        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, scratch[team]);
+        TM::sync();   // every count read before the starts overwrite them
+#pragma unroll
+        for (int j = 0; j < NBT; ++j) {
+            const int i = lane * NBT + j;
+            if (i < nb) hist[team][i] = run;
+            run += cnt[j];
+        }
+        if (lane == 0) hist[team][nb] = (uint32_t)n;
+    }
+    TM::sync();
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
+    TM::sync();
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        if (k * TEAM + lane >= n) continue;
+        const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
+        uint32_t r = s0;
+        for (uint32_t j = s0; j < s1; ++j) r += sk[team][j] < c[k] ? 1u : 0u;
+        col[o + r] = c[k];
+        val[o + r] = v[k];
     }
 }
 
@@ -1504,9 +1609,11 @@ static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
 
 // sym5 (sym5_kernels.hpp): SYM4_MAX+1 .. SYM5_MAX products, NW waves per row
 constexpr int32_t SYM5_MAX = 16384;
-template <int U, int NW>
+// sym5 over the hash-partitioned bin (PART): rows of up to SYM5P_MAX products
+constexpr int32_t SYM5P_MAX = 32768;
+template <int U, int NW, bool PART = false>
 static void sym5_launch(const Sym3Args &a, hipStream_t s) {
-    auto kern = k_sym5<U, NW, 8>;
+    auto kern = k_sym5<U, NW, 8, PART>;
     const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
 }
@@ -1762,15 +1869,12 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     int32_t *axl = as<int32_t>(bufs[B_AXL]);
     int64_t *axp = as<int64_t>(bufs[B_AXP]);
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
-    if (a_entries > 0) {
-        const int64_t per = (int64_t)AN_BLOCK * AN_U;
-        const unsigned g = (unsigned)std::min<int64_t>((a_entries + per - 1) / per, 16384);
-        k_an_entries<<<g, AN_BLOCK, 0, s>>>(A, B, a_entries,
-                                            AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, &dc->wide_b});
-    }
+    if (a_entries > 0)   // one block per scan tile (its B-row length sum -> B_PART2)
+        k_an_entries<<<(unsigned)nbe, AN_BLOCK, 0, s>>>(A, B, a_entries,
+                                                        AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, &dc->wide_b},
+                                                        as<int64_t>(bufs[B_PART2]));
     CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
-        k_scan_reduce<<<(unsigned)nbe, SCAN_BLOCK, 0, s>>>(axl, a_entries, as<int64_t>(bufs[B_PART2]), nullptr);
         k_scan_partials<<<1, 1024, 0, s>>>(as<int64_t>(bufs[B_PART2]), nbe);
         k_scan_apply<<<(unsigned)nbe, SCAN_BLOCK, 0, s>>>(axl, a_entries, as<int64_t>(bufs[B_PART2]), axp);
     } else {
@@ -1821,6 +1925,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
     IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
     if (!c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
+    if (!c1.wide_b && c1.count[ss.nval + 1] > 0) IAS_TRY(reserve(B_PDONE, sizeof(int32_t) * (size_t)(rows + 1)));
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -1855,7 +1960,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     {
         double load[NSIDE] = {};
         std::vector<std::pair<double, int>> jobs;
-        if (c1.count[sym_part] > 0) jobs.push_back({40.0 * (double)c1.part_prod, sym_part});
+        if (c1.count[sym_part] > 0) jobs.push_back({12.0 * (double)c1.part_prod, sym_part});
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
                 const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
@@ -1871,17 +1976,28 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     }
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
+        // rows of up to SYM5P_MAX products: sym5's filters with 8 waves per
+        // row (pdone marks them); the rest, and rows whose list overflows,
+        // the bucketed hash partitions below
+        int32_t *pdone = nullptr;
+        if (!c1.wide_b) {
+            pdone = as<int32_t>(bufs[B_PDONE]);
+            Sym3Args a5{ax, B.col, SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                        sa.dupn, sa.dupt, FIXBIG_CAP, DW_MAX, nullptr, nullptr, pdone, PART_DCAP_DIV};
+            sym5_launch<SYM5P_MAX, 8, true>(a5, t);
+            CHECK_LAUNCH("k_sym5 (partitioned rows)", t);
+        }
         k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
         k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
-                                                 as<PartSpan>(bufs[B_PSPAN]));
+                                                 as<PartSpan>(bufs[B_PSPAN]), pdone);
         k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]));
-        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]), pdone);
+        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm, pdone);
         k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
+                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, pdone);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
     for (int b = ss.nval; b >= 1; --b)
@@ -2224,15 +2340,16 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     BinSpec spec{};
-    spec.nval = 6;
-    const int32_t u[] = {0, 32, 128, 512, 2048, 4096, 8192};
-    for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
+    spec.nval = 5;
+    const int32_t u[] = {0, 64, 256, 1024, 4096, 8192};
+    for (int i = 0; i <= 5; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
-    // rows longer than this -> segmented radix sort (IAS_SORT_WIDE_MIN: A/B knob)
+    // rows of at least this many entries -> the wide path (column bitmap /
+    // segmented radix sort); IAS_SORT_WIDE_MIN: A/B knob
     static const int32_t wide_min_env = [] {
         const char *e = getenv("IAS_SORT_WIDE_MIN");
         const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= 8193 ? (int32_t)v : 2049;   // 8193 / 2049 / 513 / 129: 78 / 72 / 77 / 94 ms (K3' sorted)
+        return v > 0 && v <= 8193 ? (int32_t)v : 8193;
     }();
     spec.wide_min = wide_min_env;
     RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
@@ -2286,17 +2403,15 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     if (nwide > 0 && !radix && !bitmap_sort) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     int c;
     if ((c = hc.count[1]) > 0)
-        k_sort_lds<32, 32, 8><<<grid_for(c, 8), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
+        k_sort_bucket<64, 1, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
     if ((c = hc.count[2]) > 0)
-        k_sort_lds<64, 128, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(2), c, ptr, len, stride, col, val);
+        k_sort_bucket<64, 4, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(2), c, ptr, len, stride, col, val);
     if ((c = hc.count[3]) > 0)
-        k_sort_lds<256, 512, 1><<<c, 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
+        k_sort_bucket<256, 4, 1><<<c, 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
     if ((c = hc.count[4]) > 0)
-        k_sort_lds<512, 2048, 1><<<c, 512, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
+        k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
     if ((c = hc.count[5]) > 0)
-        k_sort_lds<1024, 4096, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
-    if ((c = hc.count[6]) > 0)
-        k_sort_lds<1024, 8192, 1><<<c, 1024, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
+        k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
     if ((c = nwide) > 0 && bitmap_sort) {
         char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
         double *wv = (double *)b;

@@ -61,6 +61,11 @@ struct Sym3Args {
     int32_t bm_need;           // heavy rows above this nnz get dupn -3 (global table)
     RowRef *retry;             // rows whose possible-duplicate list overflows
     int32_t *retry_count;
+    // partitioned rows (k_sym5<..., PART>): pdone[row] = 1 for a row resolved
+    // here, 0 for one left to the partition path; per-row duplicate capacity
+    // min(P / dcap_div, dcap), the partition path's list (bin_needs)
+    int32_t *pdone = nullptr;
+    int32_t dcap_div = 0;
 };
 
 template <int K>

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build the working tree's libias.so with constants changed, into
-# build_var/libias_NAME.so, for same-box A/B runs (tools/run_variants.sh).
+# build_var/libias_NAME.so, for same-box A/B runs (tools/gpu_ab.sh).
 # usage: tools/build_const.sh NAME FILE 'sed-expression' [FILE 'sed-expression' ...]
 #   e.g. tools/build_const.sh db4 sym2_kernels.hpp 's/SYM2_DB_MAX = 8/SYM2_DB_MAX = 4/'
 set -e

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build libias.so of git revision REV (default HEAD) into build_var/libias_NAME.so,
-# for same-box A/B runs against the working tree (tools/run_variants.sh).
+# for same-box A/B runs against the working tree (tools/gpu_ab.sh).
 # usage: tools/build_rev.sh NAME [REV]
 set -e
 cd "$(dirname "$0")/.."
