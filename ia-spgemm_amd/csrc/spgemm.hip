@@ -9,12 +9,12 @@
 #include "sym4_kernels.hpp"
 #include "sym5_kernels.hpp"
 #include "num2_kernels.hpp"
-#include <functional>
 #include "short_kernels.hpp"
 #include "spgemm_engine.hpp"
 #include "ias_internal.hpp"
 
 #include <algorithm>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -488,12 +488,10 @@ __global__ __launch_bounds__(PB_BLOCK) void k_part_bucket(Rows A, AxView ax, con
                                                           const int64_t *poff, const int32_t *bcol,
                                                           const RowRef *list, int32_t count,
                                                           const int64_t *pfirst, const int64_t *pboff,
-                                                          int32_t part_cap, uint2 *bucket, PartSpan *spans,
-                                                          const int32_t *pdone) {
+                                                          int32_t part_cap, uint2 *bucket, PartSpan *spans) {
     __shared__ uint32_t cnt[PB_MAXP];
     __shared__ int scratch[32];
     const RowRef ref = list[blockIdx.x];
-    if (pdone && pdone[ref.row]) return;   // resolved by k_sym5<..., PART>
     const uint32_t np = nparts_of(ref.n, part_cap);
     const int64_t it0 = pfirst[ref.row];
     const int tid = threadIdx.x;
@@ -588,15 +586,13 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
                                                         Bitmap bm, int32_t *nnz_row, uint2 *gpairs,
                                                         const int64_t *dup_off, int32_t *dupn,
                                                         int32_t div, int32_t dmax, int *overflow,
-                                                        const uint2 *bucket, const PartSpan *spans,
-                                                        const int32_t *pdone) {
+                                                        const uint2 *bucket, const PartSpan *spans) {
     __shared__ __attribute__((aligned(16))) int32_t keys[1 << LOG2S];
     __shared__ __attribute__((aligned(16))) uint32_t minp[1 << LOG2S];
     __shared__ int scratch[64];
     __shared__ uint32_t lbits[LBITS_WORDS];
     const PartItem it = items[blockIdx.x];
     const int64_t row = it.ref.row;
-    if (pdone && pdone[row]) return;
     Timer tmr;
     tmr.start();
     for (int w = threadIdx.x; w < LBITS_WORDS; w += TEAM) lbits[w] = 0u;
@@ -622,10 +618,9 @@ __global__ __launch_bounds__(TEAM) void k_symbolic_part(const int32_t *tcol, con
 
 // Exclusive popcount prefix of each partitioned row's first-touch bitmap.
 __global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32_t count,
-                                                       const int32_t *prod, Bitmap bm, const int32_t *pdone) {
+                                                       const int32_t *prod, Bitmap bm) {
     __shared__ int scratch[8];
     const int64_t row = list[blockIdx.x].row;
-    if (pdone && pdone[row]) return;
     const int64_t W = (prod[row] + 31) / 32;
     const uint32_t *bits = bm.bits + bm.off[row];
     uint32_t *pref = bm.pref + bm.off[row];
@@ -646,10 +641,9 @@ __global__ __launch_bounds__(256) void k_bitmap_prefix(const RowRef *list, int32
 __global__ __launch_bounds__(256) void k_dup_place(const RowRef *list, int32_t count, Bitmap bm,
                                                    const uint2 *gpairs, const int64_t *dup_off,
                                                    int32_t *dupn, int32_t *gdupt, int32_t div,
-                                                   int32_t dmax, const int32_t *pdone) {
+                                                   int32_t dmax) {
     const RowRef ref = list[blockIdx.x];
     const int64_t row = ref.row;
-    if (pdone && pdone[row]) return;
     const int32_t cnt = dupn[row];
     const int32_t cap = div > 0 ? min(ref.n / div, dmax) : 0;
     if (cnt > cap) {
@@ -1572,9 +1566,16 @@ static void sym3_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM3_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM3_WPB, 0, s>>>(a);
 }
-// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then sym2's 128-lane teams over
-// the rows it handed back (count read on the device)
-static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+// The sym2 teams over the rows a sym3 / sym4 / sym5 bin hands back (their
+// count read on the device) are deferred to the end of the bin's stream: a
+// retry launch needs whole CUs (up to 151 KB of LDS) and, queued right behind
+// its bin, held the stream's next bins back while it waited for them
+// (K3': 185 us per retry launch beside the other streams vs 23 us alone).
+using Deferred = std::vector<std::function<void()>>;
+
+// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then (deferred) sym2's 128-lane
+// teams over the rows it handed back
+static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
     if (upper <= 512) sym3_launch<8>(a, s);
     else if (upper <= 768) sym3_launch<12>(a, s);
     else if (upper <= 1024) sym3_launch<16>(a, s);
@@ -1583,8 +1584,10 @@ static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream
     retry.list = a.retry;
     retry.count = a.count;   // grid bound; the device count decides
     retry.count_dev = a.retry_count;
-    if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
-    else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
+    later.push_back([=] {
+        if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
+        else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
+    });
 }
 
 // sym4's one-wave long rows (sym4_kernels.hpp): rows of SYM3_MAX+1 .. SYM4_MAX
@@ -1600,32 +1603,30 @@ static void sym4_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM4_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM4_WPB, 0, s>>>(a);
 }
-static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
     retry.list = a.retry;
     retry.count_dev = a.retry_count;   // retry.count (the bin's rows) bounds the grid
     sym4_launch<SYM4_MAX>(a, s);
-    sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s);   // the 2,049 - 4,096 bins' team (cfg 6)
+    later.push_back([=] { sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s); });   // the 2,049 - 4,096 bins' team (cfg 6)
 }
 
 // sym5 (sym5_kernels.hpp): SYM4_MAX+1 .. SYM5_MAX products, NW waves per row
 constexpr int32_t SYM5_MAX = 16384;
-// sym5 over the hash-partitioned bin (PART): rows of up to SYM5P_MAX products
-constexpr int32_t SYM5P_MAX = 32768;
-template <int U, int NW, bool PART = false>
+template <int U, int NW>
 static void sym5_launch(const Sym3Args &a, hipStream_t s) {
-    auto kern = k_sym5<U, NW, 8, PART>;
+    auto kern = k_sym5<U, NW, 8>;
     const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
 }
-static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
     retry.list = a.retry;
     retry.count_dev = a.retry_count;
     if (upper <= 8192) {
         sym5_launch<8192, 2>(a, s);
-        sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s);    // the bins' team (cfg 7)
+        later.push_back([=] { sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s); });    // the bins' team (cfg 7)
     } else {
         sym5_launch<16384, 4>(a, s);
-        sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s);   // SYM2_CFG_WIDE
+        later.push_back([=] { sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s); });   // SYM2_CFG_WIDE
     }
 }
 
@@ -1925,7 +1926,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
     IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
     if (!c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
-    if (!c1.wide_b && c1.count[ss.nval + 1] > 0) IAS_TRY(reserve(B_PDONE, sizeof(int32_t) * (size_t)(rows + 1)));
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -1960,7 +1960,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     {
         double load[NSIDE] = {};
         std::vector<std::pair<double, int>> jobs;
-        if (c1.count[sym_part] > 0) jobs.push_back({12.0 * (double)c1.part_prod, sym_part});
+        if (c1.count[sym_part] > 0) jobs.push_back({40.0 * (double)c1.part_prod, sym_part});
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
                 const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
@@ -1976,30 +1976,20 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     }
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
-        // rows of up to SYM5P_MAX products: sym5's filters with 8 waves per
-        // row (pdone marks them); the rest, and rows whose list overflows,
-        // the bucketed hash partitions below
-        int32_t *pdone = nullptr;
-        if (!c1.wide_b) {
-            pdone = as<int32_t>(bufs[B_PDONE]);
-            Sym3Args a5{ax, B.col, SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
-                        sa.dupn, sa.dupt, FIXBIG_CAP, DW_MAX, nullptr, nullptr, pdone, PART_DCAP_DIV};
-            sym5_launch<SYM5P_MAX, 8, true>(a5, t);
-            CHECK_LAUNCH("k_sym5 (partitioned rows)", t);
-        }
         k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
         k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
                                                  as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
-                                                 as<PartSpan>(bufs[B_PSPAN]), pdone);
+                                                 as<PartSpan>(bufs[B_PSPAN]));
         k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
             tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]), pdone);
-        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm, pdone);
+            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]));
+        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
         k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, pdone);
+                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
+    Deferred later;
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(sym_lane[b]);
@@ -2016,7 +2006,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                                   &dc->s3_retry[b & 15]};
-                sym5_bin(u, a5, a2, t);
+                sym5_bin(u, a5, a2, t, later);
                 CHECK_LAUNCH("k_sym5", t);
                 continue;
             }
@@ -2024,7 +2014,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                                   &dc->s3_retry[b & 15]};
-                sym4_bin(a4, a2, t);
+                sym4_bin(a4, a2, t, later);
                 CHECK_LAUNCH("k_sym4", t);
                 continue;
             }
@@ -2034,13 +2024,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                   &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
                 Sym2Args r2 = a2;
                 r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
-                sym3_bin(u, a3, r2, t);
+                sym3_bin(u, a3, r2, t, later);
                 CHECK_LAUNCH("k_sym3", t);
                 continue;
             }
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);
         }
+    for (auto &f : later) f();
+    CHECK_LAUNCH("k_sym2 (retries)", s);
     HIPC(hipGetLastError());
     IAS_TRY(join());
 

@@ -68,9 +68,7 @@ struct ias_plan {
         // work units of the row-unit numeric pass (num2)
         B_N2CNT, B_N2OFF, B_N2UNIT,
         // sym3's retry lists (rows whose possible-duplicate list overflowed)
-        B_S3RETRY,
-        // partitioned rows resolved by k_sym5<..., PART> (per row: 1 = done)
-        B_PDONE, B_COUNT
+        B_S3RETRY, B_COUNT
     };
     struct Buf {
         void *p = nullptr;

@@ -61,17 +61,13 @@ struct Sym3Args {
     int32_t bm_need;           // heavy rows above this nnz get dupn -3 (global table)
     RowRef *retry;             // rows whose possible-duplicate list overflows
     int32_t *retry_count;
-    // partitioned rows (k_sym5<..., PART>): pdone[row] = 1 for a row resolved
-    // here, 0 for one left to the partition path; per-row duplicate capacity
-    // min(P / dcap_div, dcap), the partition path's list (bin_needs)
-    int32_t *pdone = nullptr;
-    int32_t dcap_div = 0;
 };
 
+constexpr int S3_F1BPP = 16;   // f1 bits per product bound (false candidates ~ P / (2 * F1B))
 template <int K>
 struct Sym3Lds {
     static constexpr int U = 64 * K;       // product bound
-    static constexpr int F1B = 16 * U;     // f1 bits
+    static constexpr int F1B = S3_F1BPP * U;   // f1 bits
     static constexpr int F1W = F1B / 32;
     static constexpr int F2B = 2 * U;      // f2 bits
     static constexpr int F2W = F2B / 32;   // >= 2K: its first words also hold the bitmap words (exact phase)

@@ -48,7 +48,6 @@ struct Sym5Lds {
         uint32_t pref[BW];                         // word prefixes (finish)
     };
     int32_t cbase[NWIN];                           // non-empty entries starting before each window
-    int32_t gsum[NE / WAVE], gne[NE / WAVE];       // per 64-entry group: products, non-empty entries
     int32_t ebase[NE];
     uint32_t words[BW];
     int32_t nl;                                    // list counter
@@ -58,13 +57,8 @@ struct Sym5Lds {
     __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
 };
 
-// PART: the rows of the hash-partitioned bin (longer than SYM5_MAX products):
-// those within U products and NE entries whose list fits are resolved here
-// (pdone = 1: bitmap and prefixes always written, as the partition path
-// writes them; duplicates beyond the row's capacity -> dupn -1, the numeric
-// partition tables), the rest are left to the partition path (pdone = 0).
-template <int U, int NW, int KC, bool PART = false>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PART ? 1 : 4))) void k_sym5(Sym3Args) {
+template <int U, int NW, int KC>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void k_sym5(Sym3Args) {
     using LDS = Sym5Lds<U, NW>;
     using TM = Team<LDS::T>;
     constexpr int T = LDS::T;
@@ -84,58 +78,38 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PART ? 
         const int32_t P = __builtin_amdgcn_readfirstlane(s3_args()->prod[row]);
         if (P > U || E > LDS::NE) {
             if (tid == 0) {
-                if constexpr (PART) {
-                    s3_args()->pdone[row] = 0;
-                } else {
-                    const int32_t j = atomicAdd(s3_args()->retry_count, 1);
-                    s3_args()->retry[j] = ref;
-                }
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
             }
             continue;
         }
         const int nwin = (P + 63) >> 6;
         const int64_t q0 = ref.q0;
         if (tid == 0) L.nl = 0;
-        // ---- entries -> ebase + start masks: 64-entry groups round robin over
-        // the waves (group sums first, then each group from its carry)
-        const int G = (E + WAVE - 1) / WAVE;
-        for (int k = tid; k < nwin; k += T) L.smask[k] = 0ull;
-        if (G > 1) {
-            for (int g = w; g < G; g += NW) {
-                const int e = g * WAVE + lane;
-                const int32_t bl = e < E ? s3_args()->ax.blen[q0 + e] : 0;
-                const int incl = wave_incl_sum(bl);
-                const uint64_t nem = __ballot(bl > 0);
-                if (lane == 0) {
-                    L.gsum[g] = __builtin_amdgcn_readlane(incl, WAVE - 1);
-                    L.gne[g] = (int)__popcll(nem);
-                }
-            }
-        }
-        __syncthreads();
-        for (int g = w; g < G; g += NW) {
-            int carry = 0, nec = 0;
-            for (int j = 0; j < g; ++j) {
-                carry += L.gsum[j];
-                nec += L.gne[j];
-            }
-            const int e = g * WAVE + lane;
-            int32_t bl = 0;
-            int64_t bs = 0;
-            if (e < E) {
-                bl = s3_args()->ax.blen[q0 + e];
-                bs = s3_args()->ax.bstart[q0 + e];
-            }
-            const int incl = wave_incl_sum(bl);
-            const int rel = carry + incl - bl;
-            const uint64_t nem = __ballot(bl > 0);
-            if (bl > 0 && rel < P) {
-                L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
-                atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
-            }
-        }
-        __syncthreads();
+        // ---- wave 0: entries -> ebase + start masks, then the window bases
         if (w == 0) {
+            for (int k = lane; k < nwin; k += WAVE) L.smask[k] = 0ull;
+            s3_sync();
+            int carry = 0, nec = 0;
+            for (int g = 0; g < E; g += WAVE) {
+                const int e = g + lane;
+                int32_t bl = 0;
+                int64_t bs = 0;
+                if (e < E) {
+                    bl = s3_args()->ax.blen[q0 + e];
+                    bs = s3_args()->ax.bstart[q0 + e];
+                }
+                const int incl = wave_incl_sum(bl);
+                const int rel = carry + incl - bl;
+                const uint64_t nem = __ballot(bl > 0);
+                if (bl > 0 && rel < P) {
+                    L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
+                    atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
+                }
+                carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
+                nec += (int)__popcll(nem);
+            }
+            s3_sync();
             // window bases: lane j takes windows j*WIN_PL .. +WIN_PL
             int cnt = 0;
 #pragma unroll
@@ -242,12 +216,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PART ? 
         const int32_t nl = L.nl;
         if (4 * nl > 3 * LDS::LC) {
             if (tid == 0) {
-                if constexpr (PART) {
-                    s3_args()->pdone[row] = 0;
-                } else {
-                    const int32_t j = atomicAdd(s3_args()->retry_count, 1);
-                    s3_args()->retry[j] = ref;
-                }
+                const int32_t j = atomicAdd(s3_args()->retry_count, 1);
+                s3_args()->retry[j] = ref;
             }
         } else {
             int2 e[LDS::LT];
@@ -322,16 +292,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PART ? 
                 }
             }
             __syncthreads();
-            const int32_t dcap = PART ? min(P / s3_args()->dcap_div, s3_args()->dcap) : s3_args()->dcap;
-            const bool heavy = P - nnz > dcap;
-            if (PART || !heavy) {
+            const bool heavy = P - nnz > s3_args()->dcap;
+            if (!heavy) {
                 const int64_t bmoff = s3_args()->bm.off[row];
                 for (int wi = tid; wi < W; wi += T) {
                     s3_args()->bm.bits[bmoff + wi] = L.words[wi];
                     s3_args()->bm.pref[bmoff + wi] = L.pref[wi];
                 }
-            }
-            if (!heavy) {
                 if (nl > 0) {
                     const int64_t dupoff = s3_args()->dup_off[row];
 #pragma unroll
@@ -347,12 +314,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PART ? 
             }
             if (tid == 0) {
                 s3_args()->nnz_row[row] = nnz;
-                if constexpr (PART) {
-                    s3_args()->dupn[row] = heavy ? -1 : P - nnz;
-                    s3_args()->pdone[row] = 1;
-                } else {
-                    s3_args()->dupn[row] = heavy ? (nnz > s3_args()->bm_need ? -3 : -1) : P - nnz;
-                }
+                s3_args()->dupn[row] = heavy ? (nnz > s3_args()->bm_need ? -3 : -1) : P - nnz;
             }
         }
         // ---- the filters empty for the next row
