@@ -985,7 +985,7 @@ __global__ void k_fill_rows(const int64_t *ptr, int64_t rows, int32_t *row_idx) 
 }
 
 // ---------------------------------------------------------------- row sort
-// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (8192 by default,
+// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (16,384 by default,
 // IAS_SORT_WIDE_MIN lowers it) get a bucket sort in LDS (k_sort_bucket).
 // Longer rows: the column bitmap sort (k_sort_bitmap) when C has at most 2^20
 // columns, else one segmented radix sort over a compact workspace
@@ -1033,43 +1033,29 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
 // into nb ~ n/4 equal parts (a monotone map, so bucket order is key order);
 // an entry's position = its bucket's start (a scan of the bucket counts) +
 // the keys of its bucket below it (a short loop over the bucket's keys,
-// which are ~4 on average: O(n) work per row, values never leave registers).
-// One read and one write of each entry, three or four team barriers per row
-// (the bitonic sort it replaces needed one per stage, log2(n)^2 / 2 of them).
-template <int TEAM, int E, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
-                                                           const int64_t *ptr, const int32_t *len,
-                                                           int64_t stride, int32_t *col, double *val) {
-    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+// which are ~4 on average: O(n) work per row).  One read and one write of
+// each entry, a handful of team barriers per row (the bitonic sort it
+// replaces needed one per stage, log2(n)^2 / 2 of them).  Bucket indices are
+// recomputed rather than kept, and each key takes its bucket slot by a second
+// atomic on a cursor copy of the starts, so the columns are the only per-entry
+// registers the ranking needs.
+template <int TEAM, int E>
+struct SortBucketLds {
+    static constexpr int CAP = TEAM * E;
+    static constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
+    int32_t sk[CAP];
+    uint32_t start[NBM + 1];   // counts, then bucket starts (+ n at nb)
+    uint32_t cur[NBM];         // scatter cursors
+    int scratch[64];
+};
+// r[k] = sorted position of c[k] (k * TEAM + lane < n) within its row
+template <int TEAM, int E>
+__device__ __forceinline__ void sort_bucket_ranks(SortBucketLds<TEAM, E> &L, const int32_t (&c)[E], int32_t n,
+                                                  int32_t lo, int32_t hi, uint32_t (&r)[E]) {
     using TM = Team<TEAM>;
-    constexpr int CAP = TEAM * E;
-    constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
-    constexpr int NBT = (NBM + TEAM - 1) / TEAM;      // bucket counts per thread in the scan
-    __shared__ int32_t sk[TPW][CAP];
-    __shared__ uint32_t hist[TPW][NBM + 1];
-    __shared__ int scratch[TPW][64];
-    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    using LDS = SortBucketLds<TEAM, E>;
+    constexpr int NBT = (LDS::NBM + TEAM - 1) / TEAM;   // bucket counts per thread in the scan
     const int lane = TM::lane();
-    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx].row : -1;
-    int64_t o = 0;
-    int32_t n = 0;
-    if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
-    int32_t c[E];
-    double v[E];
-    int32_t lo = INT32_MAX, hi = INT32_MIN;
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        const int e = k * TEAM + lane;
-        c[k] = 0;
-        v[k] = 0.0;
-        if (e < n) {
-            c[k] = col[o + e];
-            v[k] = val[o + e];
-            lo = min(lo, c[k]);
-            hi = max(hi, c[k]);
-        }
-    }
     // the row's column range (team min / max)
     {
         constexpr int W = TEAM < WAVE ? TEAM : WAVE;
@@ -1081,32 +1067,27 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
         if constexpr (TM::MULTI) {
             const int w = lane / WAVE;
             if ((lane & (WAVE - 1)) == 0) {
-                scratch[0][2 * w] = lo;
-                scratch[0][2 * w + 1] = hi;
+                L.scratch[2 * w] = lo;
+                L.scratch[2 * w + 1] = hi;
             }
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < TM::NWAVES; ++i) {
-                lo = min(lo, scratch[0][2 * i]);
-                hi = max(hi, scratch[0][2 * i + 1]);
+                lo = min(lo, L.scratch[2 * i]);
+                hi = max(hi, L.scratch[2 * i + 1]);
             }
         }
     }
     // nb: a power of two near n / 4 (at least 1, at most NBM)
     int nb = 1;
-    while (nb < NBM && 4 * nb * 2 <= n) nb <<= 1;
-    for (int i = lane; i <= nb; i += TEAM) hist[team][i] = 0u;
+    while (nb < LDS::NBM && 4 * nb * 2 <= n) nb <<= 1;
+    for (int i = lane; i <= nb; i += TEAM) L.start[i] = 0u;
     TM::sync();   // (multi-wave: also every wave's min / max read before scratch is reused)
     const float scale = n > 0 ? (float)nb / ((float)((uint32_t)(hi - lo)) + 1.0f) : 0.0f;
-    int b[E];
-    uint32_t pib[E];
+    auto bucket = [&](int32_t x) { return min((int)((float)((uint32_t)(x - lo)) * scale), nb - 1); };
 #pragma unroll
-    for (int k = 0; k < E; ++k) {
-        const int e = k * TEAM + lane;
-        b[k] = min((int)((float)((uint32_t)(c[k] - lo)) * scale), nb - 1);
-        pib[k] = 0u;
-        if (e < n) pib[k] = atomicAdd(&hist[team][b[k]], 1u);
-    }
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) atomicAdd(&L.start[bucket(c[k])], 1u);
     TM::sync();
     // bucket starts: exclusive scan of the counts (NBT per thread, in order)
     {
@@ -1114,33 +1095,128 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            cnt[j] = i < nb ? hist[team][i] : 0u;
+            cnt[j] = i < nb ? L.start[i] : 0u;
             sum += cnt[j];
         }
         int tot;
-        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, scratch[team]);
+        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, L.scratch);
         TM::sync();   // every count read before the starts overwrite them
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            if (i < nb) hist[team][i] = run;
+            if (i < nb) {
+                L.start[i] = run;
+                L.cur[i] = run;
+            }
             run += cnt[j];
         }
-        if (lane == 0) hist[team][nb] = (uint32_t)n;
+        if (lane == 0) L.start[nb] = (uint32_t)n;
     }
     TM::sync();
 #pragma unroll
     for (int k = 0; k < E; ++k)
-        if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
+        if (k * TEAM + lane < n) L.sk[atomicAdd(&L.cur[bucket(c[k])], 1u)] = c[k];
     TM::sync();
 #pragma unroll
     for (int k = 0; k < E; ++k) {
+        r[k] = 0u;
         if (k * TEAM + lane >= n) continue;
-        const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
-        uint32_t r = s0;
-        for (uint32_t j = s0; j < s1; ++j) r += sk[team][j] < c[k] ? 1u : 0u;
-        col[o + r] = c[k];
-        val[o + r] = v[k];
+        const int b = bucket(c[k]);
+        const uint32_t s0 = L.start[b], s1 = L.start[b + 1];
+        uint32_t x = s0;
+        for (uint32_t j = s0; j < s1; ++j) x += L.sk[j] < c[k] ? 1u : 0u;
+        r[k] = x;
+    }
+}
+
+// One row per team, in place: the values wait in registers for the ranks.
+template <int TEAM, int E, int TPW>
+__global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
+                                                           const int64_t *ptr, const int32_t *len,
+                                                           int64_t stride, int32_t *col, double *val) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
+    __shared__ SortBucketLds<TEAM, E> lds[TPW];
+    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    const int lane = Team<TEAM>::lane();
+    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
+    const int64_t row = idx < count ? list[idx].row : -1;
+    int64_t o = 0;
+    int32_t n = 0;
+    if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
+    int32_t *const rc = col + o;   // the row's arrays (32-bit per-lane offsets)
+    double *const rv = val + o;
+    int32_t c[E];
+    double v[E];
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        c[k] = 0;
+        v[k] = 0.0;
+        if (e < n) {
+            c[k] = rc[e];
+            v[k] = rv[e];
+            lo = min(lo, c[k]);
+            hi = max(hi, c[k]);
+        }
+    }
+    uint32_t r[E];
+    sort_bucket_ranks<TEAM, E>(lds[team], c, n, lo, hi, r);
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) {
+            rc[r[k]] = c[k];
+            rv[r[k]] = v[k];
+        }
+}
+
+// Rows of up to 1024 * 16 entries (too many values for registers): ranked
+// from the columns alone, each value read again and placed in a per-workgroup
+// staging row (L2-resident, 12 B per entry), which is then copied back.
+// Persistent workgroups, one row at a time.
+constexpr int SORTW_T = 1024, SORTW_E = 16;
+__global__ __launch_bounds__(SORTW_T) void k_sort_bucket_ws(const RowRef *list, int32_t count, const int64_t *ptr,
+                                                            const int32_t *len, int64_t stride, int32_t *col,
+                                                            double *val, int32_t *wcol, double *wval) {
+    constexpr int CAP = SORTW_T * SORTW_E;
+    __shared__ SortBucketLds<SORTW_T, SORTW_E> L;
+    const int lane = (int)threadIdx.x;
+    int32_t *const sc = wcol + (int64_t)blockIdx.x * CAP;
+    double *const sv = wval + (int64_t)blockIdx.x * CAP;
+    for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        int64_t o;
+        int32_t n;
+        sort_row_span(ptr, len, stride, list[idx].row, o, n);
+        int32_t *const rc = col + o;
+        double *const rv = val + o;
+        int32_t c[SORTW_E];
+        int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+        for (int k = 0; k < SORTW_E; ++k) {
+            const int e = k * SORTW_T + lane;
+            c[k] = e < n ? rc[e] : 0;
+            if (e < n) {
+                lo = min(lo, c[k]);
+                hi = max(hi, c[k]);
+            }
+        }
+        uint32_t r[SORTW_E];
+        sort_bucket_ranks<SORTW_T, SORTW_E>(L, c, n, lo, hi, r);
+#pragma unroll
+        for (int k = 0; k < SORTW_E; ++k) {
+            const int e = k * SORTW_T + lane;
+            if (e < n) {
+                sc[r[k]] = c[k];
+                sv[r[k]] = rv[e];
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        for (int e = lane; e < n; e += SORTW_T) {
+            rc[e] = sc[e];
+            rv[e] = sv[e];
+        }
+        __syncthreads();   // the staging row and L free for the next row
     }
 }
 
@@ -1566,16 +1642,9 @@ static void sym3_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM3_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM3_WPB, 0, s>>>(a);
 }
-// The sym2 teams over the rows a sym3 / sym4 / sym5 bin hands back (their
-// count read on the device) are deferred to the end of the bin's stream: a
-// retry launch needs whole CUs (up to 151 KB of LDS) and, queued right behind
-// its bin, held the stream's next bins back while it waited for them
-// (K3': 185 us per retry launch beside the other streams vs 23 us alone).
-using Deferred = std::vector<std::function<void()>>;
-
-// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then (deferred) sym2's 128-lane
-// teams over the rows it handed back
-static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
+// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then sym2's 128-lane teams over
+// the rows it handed back (count read on the device)
+static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
     if (upper <= 512) sym3_launch<8>(a, s);
     else if (upper <= 768) sym3_launch<12>(a, s);
     else if (upper <= 1024) sym3_launch<16>(a, s);
@@ -1584,10 +1653,8 @@ static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream
     retry.list = a.retry;
     retry.count = a.count;   // grid bound; the device count decides
     retry.count_dev = a.retry_count;
-    later.push_back([=] {
-        if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
-        else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
-    });
+    if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
+    else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
 }
 
 // sym4's one-wave long rows (sym4_kernels.hpp): rows of SYM3_MAX+1 .. SYM4_MAX
@@ -1603,11 +1670,11 @@ static void sym4_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM4_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM4_WPB, 0, s>>>(a);
 }
-static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
+static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
     retry.list = a.retry;
     retry.count_dev = a.retry_count;   // retry.count (the bin's rows) bounds the grid
     sym4_launch<SYM4_MAX>(a, s);
-    later.push_back([=] { sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s); });   // the 2,049 - 4,096 bins' team (cfg 6)
+    sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s);   // the 2,049 - 4,096 bins' team (cfg 6)
 }
 
 // sym5 (sym5_kernels.hpp): SYM4_MAX+1 .. SYM5_MAX products, NW waves per row
@@ -1618,15 +1685,15 @@ static void sym5_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
 }
-static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s, Deferred &later) {
+static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
     retry.list = a.retry;
     retry.count_dev = a.retry_count;
     if (upper <= 8192) {
         sym5_launch<8192, 2>(a, s);
-        later.push_back([=] { sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s); });    // the bins' team (cfg 7)
+        sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s);    // the bins' team (cfg 7)
     } else {
         sym5_launch<16384, 4>(a, s);
-        later.push_back([=] { sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s); });   // SYM2_CFG_WIDE
+        sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s);   // SYM2_CFG_WIDE
     }
 }
 
@@ -1989,7 +2056,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                       sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
         CHECK_LAUNCH("k_symbolic_part", t);
     }
-    Deferred later;
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(sym_lane[b]);
@@ -2006,7 +2072,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                                   &dc->s3_retry[b & 15]};
-                sym5_bin(u, a5, a2, t, later);
+                sym5_bin(u, a5, a2, t);
                 CHECK_LAUNCH("k_sym5", t);
                 continue;
             }
@@ -2014,7 +2080,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                                   sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                                   &dc->s3_retry[b & 15]};
-                sym4_bin(a4, a2, t, later);
+                sym4_bin(a4, a2, t);
                 CHECK_LAUNCH("k_sym4", t);
                 continue;
             }
@@ -2024,15 +2090,13 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                   &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
                 Sym2Args r2 = a2;
                 r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
-                sym3_bin(u, a3, r2, t, later);
+                sym3_bin(u, a3, r2, t);
                 CHECK_LAUNCH("k_sym3", t);
                 continue;
             }
             sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
             CHECK_LAUNCH("k_sym2", t);
         }
-    for (auto &f : later) f();
-    CHECK_LAUNCH("k_sym2 (retries)", s);
     HIPC(hipGetLastError());
     IAS_TRY(join());
 
@@ -2332,16 +2396,16 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     BinSpec spec{};
-    spec.nval = 5;
-    const int32_t u[] = {0, 64, 256, 1024, 4096, 8192};
-    for (int i = 0; i <= 5; ++i) spec.upper[i] = u[i];
+    spec.nval = 6;
+    const int32_t u[] = {0, 64, 256, 1024, 4096, 8192, 16384};
+    for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
     // rows of at least this many entries -> the wide path (column bitmap /
     // segmented radix sort); IAS_SORT_WIDE_MIN: A/B knob
     static const int32_t wide_min_env = [] {
         const char *e = getenv("IAS_SORT_WIDE_MIN");
         const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= 8193 ? (int32_t)v : 8193;
+        return v > 0 && v <= 16385 ? (int32_t)v : 16385;
     }();
     spec.wide_min = wide_min_env;
     RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
@@ -2404,6 +2468,14 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
         k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
     if ((c = hc.count[5]) > 0)
         k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
+    if ((c = hc.count[6]) > 0) {   // (the column bitmap sort took ~2.5x as long on these rows)
+        const int64_t g = std::min<int64_t>(c, resident_blocks(k_sort_bucket_ws, SORTW_T, 0));
+        IAS_TRY(plan->reserve(ias_plan::B_TMP6, 12ull * (uint64_t)g * SORTW_T * SORTW_E));
+        int32_t *wc = (int32_t *)plan->bufs[ias_plan::B_TMP6].p;
+        double *wv = (double *)(wc + g * SORTW_T * SORTW_E);
+        k_sort_bucket_ws<<<(unsigned)std::max<int64_t>(g, 1), SORTW_T, 0, s>>>(lst(6), c, ptr, len, stride, col,
+                                                                                 val, wc, wv);
+    }
     if ((c = nwide) > 0 && bitmap_sort) {
         char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
         double *wv = (double *)b;

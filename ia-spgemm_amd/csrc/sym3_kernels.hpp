@@ -63,7 +63,7 @@ struct Sym3Args {
     int32_t *retry_count;
 };
 
-constexpr int S3_F1BPP = 16;   // f1 bits per product bound (false candidates ~ P / (2 * F1B))
+constexpr int S3_F1BPP = 32;   // f1 bits per product bound (false candidates ~ P / (2 * F1B)); 16: K3' symbolic 4.03-4.07 vs 3.98-4.02 ms
 template <int K>
 struct Sym3Lds {
     static constexpr int U = 64 * K;       // product bound
