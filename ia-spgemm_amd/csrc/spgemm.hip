@@ -985,7 +985,7 @@ __global__ void k_fill_rows(const int64_t *ptr, int64_t rows, int32_t *row_idx) 
 }
 
 // ---------------------------------------------------------------- row sort
-// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (16,384 by default,
+// IAS_ORDER_SORTED: rows up to `wide_min` - 1 entries (8,192 by default,
 // IAS_SORT_WIDE_MIN lowers it) get a bucket sort in LDS (k_sort_bucket).
 // Longer rows: the column bitmap sort (k_sort_bitmap) when C has at most 2^20
 // columns, else one segmented radix sort over a compact workspace
@@ -1033,29 +1033,44 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
 // into nb ~ n/4 equal parts (a monotone map, so bucket order is key order);
 // an entry's position = its bucket's start (a scan of the bucket counts) +
 // the keys of its bucket below it (a short loop over the bucket's keys,
-// which are ~4 on average: O(n) work per row).  One read and one write of
-// each entry, a handful of team barriers per row (the bitonic sort it
-// replaces needed one per stage, log2(n)^2 / 2 of them).  Bucket indices are
-// recomputed rather than kept, and each key takes its bucket slot by a second
-// atomic on a cursor copy of the starts, so the columns are the only per-entry
-// registers the ranking needs.
-template <int TEAM, int E>
-struct SortBucketLds {
-    static constexpr int CAP = TEAM * E;
-    static constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
-    int32_t sk[CAP];
-    uint32_t start[NBM + 1];   // counts, then bucket starts (+ n at nb)
-    uint32_t cur[NBM];         // scatter cursors
-    int scratch[64];
-};
-// r[k] = sorted position of c[k] (k * TEAM + lane < n) within its row
-template <int TEAM, int E>
-__device__ __forceinline__ void sort_bucket_ranks(SortBucketLds<TEAM, E> &L, const int32_t (&c)[E], int32_t n,
-                                                  int32_t lo, int32_t hi, uint32_t (&r)[E]) {
+// which are ~4 on average: O(n) work per row, values never leave registers).
+// One read and one write of each entry, three or four team barriers per row
+// (the bitonic sort it replaces needed one per stage, log2(n)^2 / 2 of them).
+template <int TEAM, int E, int TPW>
+__global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
+                                                           const int64_t *ptr, const int32_t *len,
+                                                           int64_t stride, int32_t *col, double *val) {
+    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     using TM = Team<TEAM>;
-    using LDS = SortBucketLds<TEAM, E>;
-    constexpr int NBT = (LDS::NBM + TEAM - 1) / TEAM;   // bucket counts per thread in the scan
+    constexpr int CAP = TEAM * E;
+    constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
+    constexpr int NBT = (NBM + TEAM - 1) / TEAM;      // bucket counts per thread in the scan
+    __shared__ int32_t sk[TPW][CAP];
+    __shared__ double sv[TPW][CAP];   // the sorted row, written out coalesced
+    __shared__ uint32_t hist[TPW][NBM + 1];
+    __shared__ int scratch[TPW][64];
+    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
     const int lane = TM::lane();
+    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
+    const int64_t row = idx < count ? list[idx].row : -1;
+    int64_t o = 0;
+    int32_t n = 0;
+    if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
+    int32_t c[E];
+    double v[E];
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        c[k] = 0;
+        v[k] = 0.0;
+        if (e < n) {
+            c[k] = col[o + e];
+            v[k] = val[o + e];
+            lo = min(lo, c[k]);
+            hi = max(hi, c[k]);
+        }
+    }
     // the row's column range (team min / max)
     {
         constexpr int W = TEAM < WAVE ? TEAM : WAVE;
@@ -1067,27 +1082,32 @@ __device__ __forceinline__ void sort_bucket_ranks(SortBucketLds<TEAM, E> &L, con
         if constexpr (TM::MULTI) {
             const int w = lane / WAVE;
             if ((lane & (WAVE - 1)) == 0) {
-                L.scratch[2 * w] = lo;
-                L.scratch[2 * w + 1] = hi;
+                scratch[0][2 * w] = lo;
+                scratch[0][2 * w + 1] = hi;
             }
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < TM::NWAVES; ++i) {
-                lo = min(lo, L.scratch[2 * i]);
-                hi = max(hi, L.scratch[2 * i + 1]);
+                lo = min(lo, scratch[0][2 * i]);
+                hi = max(hi, scratch[0][2 * i + 1]);
             }
         }
     }
     // nb: a power of two near n / 4 (at least 1, at most NBM)
     int nb = 1;
-    while (nb < LDS::NBM && 4 * nb * 2 <= n) nb <<= 1;
-    for (int i = lane; i <= nb; i += TEAM) L.start[i] = 0u;
+    while (nb < NBM && 4 * nb * 2 <= n) nb <<= 1;
+    for (int i = lane; i <= nb; i += TEAM) hist[team][i] = 0u;
     TM::sync();   // (multi-wave: also every wave's min / max read before scratch is reused)
     const float scale = n > 0 ? (float)nb / ((float)((uint32_t)(hi - lo)) + 1.0f) : 0.0f;
-    auto bucket = [&](int32_t x) { return min((int)((float)((uint32_t)(x - lo)) * scale), nb - 1); };
+    int b[E];
+    uint32_t pib[E];
 #pragma unroll
-    for (int k = 0; k < E; ++k)
-        if (k * TEAM + lane < n) atomicAdd(&L.start[bucket(c[k])], 1u);
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        b[k] = min((int)((float)((uint32_t)(c[k] - lo)) * scale), nb - 1);
+        pib[k] = 0u;
+        if (e < n) pib[k] = atomicAdd(&hist[team][b[k]], 1u);
+    }
     TM::sync();
     // bucket starts: exclusive scan of the counts (NBT per thread, in order)
     {
@@ -1095,128 +1115,49 @@ __device__ __forceinline__ void sort_bucket_ranks(SortBucketLds<TEAM, E> &L, con
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            cnt[j] = i < nb ? L.start[i] : 0u;
+            cnt[j] = i < nb ? hist[team][i] : 0u;
             sum += cnt[j];
         }
         int tot;
-        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, L.scratch);
+        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, scratch[team]);
         TM::sync();   // every count read before the starts overwrite them
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            if (i < nb) {
-                L.start[i] = run;
-                L.cur[i] = run;
-            }
+            if (i < nb) hist[team][i] = run;
             run += cnt[j];
         }
-        if (lane == 0) L.start[nb] = (uint32_t)n;
+        if (lane == 0) hist[team][nb] = (uint32_t)n;
     }
     TM::sync();
 #pragma unroll
     for (int k = 0; k < E; ++k)
-        if (k * TEAM + lane < n) L.sk[atomicAdd(&L.cur[bucket(c[k])], 1u)] = c[k];
+        if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
     TM::sync();
+    uint32_t r[E];
 #pragma unroll
     for (int k = 0; k < E; ++k) {
         r[k] = 0u;
         if (k * TEAM + lane >= n) continue;
-        const int b = bucket(c[k]);
-        const uint32_t s0 = L.start[b], s1 = L.start[b + 1];
+        const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
         uint32_t x = s0;
-        for (uint32_t j = s0; j < s1; ++j) x += L.sk[j] < c[k] ? 1u : 0u;
+        for (uint32_t j = s0; j < s1; ++j) x += sk[team][j] < c[k] ? 1u : 0u;
         r[k] = x;
     }
-}
-
-// One row per team, in place: the values wait in registers for the ranks.
-template <int TEAM, int E, int TPW>
-__global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
-                                                           const int64_t *ptr, const int32_t *len,
-                                                           int64_t stride, int32_t *col, double *val) {
-    static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
-    __shared__ SortBucketLds<TEAM, E> lds[TPW];
-    const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
-    const int lane = Team<TEAM>::lane();
-    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx].row : -1;
-    int64_t o = 0;
-    int32_t n = 0;
-    if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
-    int32_t *const rc = col + o;   // the row's arrays (32-bit per-lane offsets)
-    double *const rv = val + o;
-    int32_t c[E];
-    double v[E];
-    int32_t lo = INT32_MAX, hi = INT32_MIN;
-#pragma unroll
-    for (int k = 0; k < E; ++k) {
-        const int e = k * TEAM + lane;
-        c[k] = 0;
-        v[k] = 0.0;
-        if (e < n) {
-            c[k] = rc[e];
-            v[k] = rv[e];
-            lo = min(lo, c[k]);
-            hi = max(hi, c[k]);
-        }
-    }
-    uint32_t r[E];
-    sort_bucket_ranks<TEAM, E>(lds[team], c, n, lo, hi, r);
+    // the entries land at their ranks in LDS, then leave in order: a lane's
+    // scattered global store touched its own cache line (one lane per cycle
+    // in the texture unit), these are contiguous
+    TM::sync();   // every rank read of sk done
 #pragma unroll
     for (int k = 0; k < E; ++k)
         if (k * TEAM + lane < n) {
-            rc[r[k]] = c[k];
-            rv[r[k]] = v[k];
+            sk[team][r[k]] = c[k];
+            sv[team][r[k]] = v[k];
         }
-}
-
-// Rows of up to 1024 * 16 entries (too many values for registers): ranked
-// from the columns alone, each value read again and placed in a per-workgroup
-// staging row (L2-resident, 12 B per entry), which is then copied back.
-// Persistent workgroups, one row at a time.
-constexpr int SORTW_T = 1024, SORTW_E = 16;
-__global__ __launch_bounds__(SORTW_T) void k_sort_bucket_ws(const RowRef *list, int32_t count, const int64_t *ptr,
-                                                            const int32_t *len, int64_t stride, int32_t *col,
-                                                            double *val, int32_t *wcol, double *wval) {
-    constexpr int CAP = SORTW_T * SORTW_E;
-    __shared__ SortBucketLds<SORTW_T, SORTW_E> L;
-    const int lane = (int)threadIdx.x;
-    int32_t *const sc = wcol + (int64_t)blockIdx.x * CAP;
-    double *const sv = wval + (int64_t)blockIdx.x * CAP;
-    for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
-        int64_t o;
-        int32_t n;
-        sort_row_span(ptr, len, stride, list[idx].row, o, n);
-        int32_t *const rc = col + o;
-        double *const rv = val + o;
-        int32_t c[SORTW_E];
-        int32_t lo = INT32_MAX, hi = INT32_MIN;
-#pragma unroll
-        for (int k = 0; k < SORTW_E; ++k) {
-            const int e = k * SORTW_T + lane;
-            c[k] = e < n ? rc[e] : 0;
-            if (e < n) {
-                lo = min(lo, c[k]);
-                hi = max(hi, c[k]);
-            }
-        }
-        uint32_t r[SORTW_E];
-        sort_bucket_ranks<SORTW_T, SORTW_E>(L, c, n, lo, hi, r);
-#pragma unroll
-        for (int k = 0; k < SORTW_E; ++k) {
-            const int e = k * SORTW_T + lane;
-            if (e < n) {
-                sc[r[k]] = c[k];
-                sv[r[k]] = rv[e];
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-        for (int e = lane; e < n; e += SORTW_T) {
-            rc[e] = sc[e];
-            rv[e] = sv[e];
-        }
-        __syncthreads();   // the staging row and L free for the next row
+    TM::sync();
+    for (int e = lane; e < n; e += TEAM) {
+        col[o + e] = sk[team][e];
+        val[o + e] = sv[team][e];
     }
 }
 
@@ -2396,16 +2337,16 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     BinSpec spec{};
-    spec.nval = 6;
-    const int32_t u[] = {0, 64, 256, 1024, 4096, 8192, 16384};
-    for (int i = 0; i <= 6; ++i) spec.upper[i] = u[i];
+    spec.nval = 7;
+    const int32_t u[] = {0, 64, 256, 512, 1024, 2048, 4096, 8192};
+    for (int i = 0; i <= 7; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
     // rows of at least this many entries -> the wide path (column bitmap /
     // segmented radix sort); IAS_SORT_WIDE_MIN: A/B knob
     static const int32_t wide_min_env = [] {
         const char *e = getenv("IAS_SORT_WIDE_MIN");
         const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= 16385 ? (int32_t)v : 16385;
+        return v > 0 && v <= 8193 ? (int32_t)v : 8193;
     }();
     spec.wide_min = wide_min_env;
     RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
@@ -2458,24 +2399,22 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     if (bitmap_sort && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * slots + 16ull * nwide + 256));
     if (nwide > 0 && !radix && !bitmap_sort) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     int c;
+    // one wave per row up to 512 entries (4 rows per workgroup, wave
+    // barriers only), then teams sized so a row fills ~half their slots
     if ((c = hc.count[1]) > 0)
         k_sort_bucket<64, 1, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
     if ((c = hc.count[2]) > 0)
         k_sort_bucket<64, 4, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(2), c, ptr, len, stride, col, val);
     if ((c = hc.count[3]) > 0)
-        k_sort_bucket<256, 4, 1><<<c, 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
+        k_sort_bucket<64, 8, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
     if ((c = hc.count[4]) > 0)
-        k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
+        k_sort_bucket<128, 8, 1><<<c, 128, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
     if ((c = hc.count[5]) > 0)
-        k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
-    if ((c = hc.count[6]) > 0) {   // (the column bitmap sort took ~2.5x as long on these rows)
-        const int64_t g = std::min<int64_t>(c, resident_blocks(k_sort_bucket_ws, SORTW_T, 0));
-        IAS_TRY(plan->reserve(ias_plan::B_TMP6, 12ull * (uint64_t)g * SORTW_T * SORTW_E));
-        int32_t *wc = (int32_t *)plan->bufs[ias_plan::B_TMP6].p;
-        double *wv = (double *)(wc + g * SORTW_T * SORTW_E);
-        k_sort_bucket_ws<<<(unsigned)std::max<int64_t>(g, 1), SORTW_T, 0, s>>>(lst(6), c, ptr, len, stride, col,
-                                                                                 val, wc, wv);
-    }
+        k_sort_bucket<256, 8, 1><<<c, 256, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
+    if ((c = hc.count[6]) > 0)
+        k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
+    if ((c = hc.count[7]) > 0)
+        k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(7), c, ptr, len, stride, col, val);
     if ((c = nwide) > 0 && bitmap_sort) {
         char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
         double *wv = (double *)b;

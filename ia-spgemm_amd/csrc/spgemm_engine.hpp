@@ -62,7 +62,7 @@ struct ias_plan {
     enum {
         B_AXS, B_AXL, B_AXV, B_AXP, B_POFF, B_TCOL, B_DUPV, B_PART2, B_PROD, B_NNZ, B_SLIST, B_NLIST, B_SITEM, B_NITEM, B_BMOFF, B_BITS, B_BPREF, B_WSOFF,
         B_CNT, B_CNT2, B_PTR, B_PART, B_WS, B_DUPOFF, B_DUPN, B_DUPT, B_DUPP,
-        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5, B_TMP6,
+        B_TMP0, B_TMP1, B_TMP2, B_TMP3, B_TMP4, B_TMP5,
         // partition buckets of the symbolic pass
         B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
         // work units of the row-unit numeric pass (num2)
