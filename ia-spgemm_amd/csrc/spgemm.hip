@@ -1045,8 +1045,12 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
     constexpr int CAP = TEAM * E;
     constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
     constexpr int NBT = (NBM + TEAM - 1) / TEAM;      // bucket counts per thread in the scan
+    // the sorted row staged in LDS and written out contiguously, except for
+    // the 1024-lane teams (the staging's 64 KB leave one team per CU: 2.03 vs
+    // 1.79 ms on K3''s 4,097 - 8,192-entry rows)
+    constexpr bool STAGE = TEAM < 1024;
     __shared__ int32_t sk[TPW][CAP];
-    __shared__ double sv[TPW][CAP];   // the sorted row, written out coalesced
+    __shared__ double sv[TPW][STAGE ? CAP : 1];
     __shared__ uint32_t hist[TPW][NBM + 1];
     __shared__ int scratch[TPW][64];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
@@ -1144,20 +1148,30 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
         for (uint32_t j = s0; j < s1; ++j) x += sk[team][j] < c[k] ? 1u : 0u;
         r[k] = x;
     }
-    // the entries land at their ranks in LDS, then leave in order: a lane's
-    // scattered global store touched its own cache line (one lane per cycle
-    // in the texture unit), these are contiguous
-    TM::sync();   // every rank read of sk done
+    if constexpr (!STAGE) {
 #pragma unroll
-    for (int k = 0; k < E; ++k)
-        if (k * TEAM + lane < n) {
-            sk[team][r[k]] = c[k];
-            sv[team][r[k]] = v[k];
+        for (int k = 0; k < E; ++k)
+            if (k * TEAM + lane < n) {
+                col[o + r[k]] = c[k];
+                val[o + r[k]] = v[k];
+            }
+    } else {
+        // the entries land at their ranks in LDS, then leave in order: a
+        // lane's scattered global store touched its own cache line (one lane
+        // per cycle in the texture unit), these are contiguous (K3' sorted
+        // 22.0 -> 21.0 ms)
+        TM::sync();   // every rank read of sk done
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+            if (k * TEAM + lane < n) {
+                sk[team][r[k]] = c[k];
+                sv[team][r[k]] = v[k];
+            }
+        TM::sync();
+        for (int e = lane; e < n; e += TEAM) {
+            col[o + e] = sk[team][e];
+            val[o + e] = sv[team][e];
         }
-    TM::sync();
-    for (int e = lane; e < n; e += TEAM) {
-        col[o + e] = sk[team][e];
-        val[o + e] = sv[team][e];
     }
 }
 
@@ -1256,6 +1270,95 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, in
             val[o + e] = wval[w0 + e];
         }
         __syncthreads();
+    }
+}
+
+// Rows of 8,193 .. 16,384 entries (C has at most SORTBM_COLS columns): the
+// column bitmap sort with the row held in registers (16 entries per lane,
+// loaded once — the loop form above reloads them per phase, a global round
+// trip each) and the sorted row staged in LDS over the dead bitmap, 8,192
+// entries at a time, then written out contiguously in place.
+constexpr int SORTB2_E = 16, SORTB2_CH = 8192;
+constexpr size_t sortb2_lds(int32_t cols) {
+    const size_t bm = 4ull * (((size_t)cols + 255) / 256 * 8);
+    const size_t st = 12ull * SORTB2_CH;
+    return (bm > st ? bm : st) + 4ull * (((size_t)cols + 255) / 256 + 1) + 4ull * 64;
+}
+__global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap16(const RowRef *list, int32_t count, const int64_t *ptr,
+                                                           const int32_t *len, int64_t stride, int32_t *col,
+                                                           double *val, int32_t ncols) {
+    extern __shared__ uint32_t sbm[];
+    const int NW = (ncols + 255) / 256 * 8;   // bitmap words, a multiple of 8
+    const size_t area = sortb2_lds(ncols) - 4ull * (NW / 8 + 1) - 4ull * 64;   // bitmap / staging bytes
+    uint32_t *bits = sbm;
+    int32_t *skey = (int32_t *)sbm;                       // staging (after the bitmap is dead)
+    double *sval = (double *)(sbm + SORTB2_CH);
+    int32_t *pre8 = (int32_t *)((char *)sbm + area);
+    int *scratch = pre8 + NW / 8 + 1;
+    const int tid = (int)threadIdx.x;
+    const int per = (NW + SORTBM_T - 1) / SORTBM_T;
+    for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        int64_t o;
+        int32_t n;
+        sort_row_span(ptr, len, stride, list[idx].row, o, n);
+        int32_t *const rc = col + o;
+        double *const rv = val + o;
+        int32_t c[SORTB2_E];
+        double v[SORTB2_E];
+#pragma unroll
+        for (int k = 0; k < SORTB2_E; ++k) {
+            const int e = k * SORTBM_T + tid;
+            c[k] = e < n ? rc[e] : 0;
+            v[k] = e < n ? rv[e] : 0.0;
+        }
+        for (int i = tid; i < NW / 4; i += SORTBM_T) ((uint4 *)bits)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < SORTB2_E; ++k)
+            if (k * SORTBM_T + tid < n) atomicOr(&bits[(uint32_t)c[k] >> 5], 1u << (c[k] & 31));
+        __syncthreads();
+        int cnt = 0;
+        for (int j = 0; j < per; ++j) {
+            const int wi = tid * per + j;
+            cnt += wi < NW ? __popc(bits[wi]) : 0;
+        }
+        int tot;
+        int run = Team<SORTBM_T>::excl_sum(cnt, tot, scratch);
+        for (int j = 0; j < per; ++j) {
+            const int wi = tid * per + j;
+            if (wi < NW) {
+                if ((wi & 7) == 0) pre8[wi >> 3] = run;
+                run += __popc(bits[wi]);
+            }
+        }
+        __syncthreads();
+        int32_t pos[SORTB2_E];
+#pragma unroll
+        for (int k = 0; k < SORTB2_E; ++k) {
+            pos[k] = 0;
+            if (k * SORTBM_T + tid < n) {
+                const uint32_t cc = (uint32_t)c[k], wi = cc >> 5;
+                int p = pre8[wi >> 3] + __popc(bits[wi] & ((1u << (cc & 31)) - 1u));
+                for (uint32_t q = wi & ~7u; q < wi; ++q) p += __popc(bits[q]);
+                pos[k] = p;
+            }
+        }
+        __syncthreads();   // every bitmap read done: the area becomes the staging row
+        for (int32_t lo = 0; lo < n; lo += SORTB2_CH) {
+            const int32_t m = min(SORTB2_CH, n - lo);
+#pragma unroll
+            for (int k = 0; k < SORTB2_E; ++k)
+                if (k * SORTBM_T + tid < n && pos[k] >= lo && pos[k] < lo + m) {
+                    skey[pos[k] - lo] = c[k];
+                    sval[pos[k] - lo] = v[k];
+                }
+            __syncthreads();
+            for (int e = tid; e < m; e += SORTBM_T) {
+                rc[lo + e] = skey[e];
+                rv[lo + e] = sval[e];
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -2337,18 +2440,20 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     Counters *dc = (Counters *)plan->bufs[ias_plan::B_TMP3].p;
     HIPC(hipMemsetAsync(dc, 0, sizeof(Counters), s));
     BinSpec spec{};
-    spec.nval = 7;
-    const int32_t u[] = {0, 64, 256, 512, 1024, 2048, 4096, 8192};
-    for (int i = 0; i <= 7; ++i) spec.upper[i] = u[i];
+    spec.nval = 8;
+    const int32_t u[] = {0, 64, 256, 512, 1024, 2048, 4096, 8192, 16384};
+    for (int i = 0; i <= 8; ++i) spec.upper[i] = u[i];
     spec.part_cap = 1;
     // rows of at least this many entries -> the wide path (column bitmap /
     // segmented radix sort); IAS_SORT_WIDE_MIN: A/B knob
     static const int32_t wide_min_env = [] {
         const char *e = getenv("IAS_SORT_WIDE_MIN");
         const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= 8193 ? (int32_t)v : 8193;
+        return v > 0 && v <= 16385 ? (int32_t)v : 16385;
     }();
-    spec.wide_min = wide_min_env;
+    // the 8,193 .. 16,384 bin is the register bitmap sort: C's columns must fit
+    // its bitmap, else those rows go to the wide path too
+    spec.wide_min = plan->n_cols > 0 && plan->n_cols <= SORTBM_COLS ? wide_min_env : std::min(wide_min_env, 8193);
     RowRef *lists = (RowRef *)plan->bufs[ias_plan::B_TMP1].p;
     int64_t *offs = (int64_t *)plan->bufs[ias_plan::B_TMP2].p;
     // the scatter's row extents are not used by the sort kernels (they read ptr/len)
@@ -2415,6 +2520,14 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
         k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
     if ((c = hc.count[7]) > 0)
         k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(7), c, ptr, len, stride, col, val);
+    if ((c = hc.count[8]) > 0) {
+        const size_t lds = sortb2_lds((int32_t)plan->n_cols);
+        static bool b2_done = false;
+        allow_lds(k_sort_bitmap16, b2_done, lds);
+        const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap16, SORTBM_T, lds));
+        k_sort_bitmap16<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, s>>>(lst(8), c, ptr, len, stride, col,
+                                                                                     val, (int32_t)plan->n_cols);
+    }
     if ((c = nwide) > 0 && bitmap_sort) {
         char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
         double *wv = (double *)b;
