@@ -244,9 +244,26 @@ __device__ __forceinline__ int32_t ent2_of(const BinSpec &sp, const Rows &A, int
     return n > INT32_MAX / sp.ent_key ? INT32_MAX : sp.ent_key * n;
 }
 
+// A row's first entry in the expanded A (clamped; a row pointer that
+// disagrees with the declared entry count sets the overflow flag).
+__device__ __forceinline__ int64_t row_q(const Rows &A, int64_t r, int64_t n_entries, Counters *cnt) {
+    int64_t s;
+    int32_t n;
+    A.row(r, s, n);
+    int64_t q = s - A.base();
+    if (q < 0 || n < 0 || q + n > n_entries) {
+        cnt->overflow = 1;
+        q = q < 0 ? 0 : (q > n_entries ? n_entries : q);
+    }
+    return q;
+}
+
+// Per row: the product offset poff (from axp at the row's first entry), the
+// products, the symbolic bin histogram, max products, flops.
 template <int RPT>
-__global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int64_t rows, int32_t *prod,
-                                                       BinSpec spec, Counters *cnt, Rows A) {
+__global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *axp, int64_t n_entries, int64_t *poff,
+                                                       int64_t rows, int32_t *prod, BinSpec spec, Counters *cnt,
+                                                       Rows A) {
     int b[RPT];
     int32_t k[RPT];
     int mx = 0;
@@ -256,7 +273,11 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
         b[i] = -1;
         k[i] = 0;
         if (r < rows) {
-            const int64_t p = poff[r + 1] - poff[r];
+            const int64_t p0 = axp[row_q(A, r, n_entries, cnt)];
+            const int64_t p1 = r + 1 < rows ? axp[row_q(A, r + 1, n_entries, cnt)] : axp[n_entries];
+            poff[r] = p0;
+            if (r + 1 == rows) poff[rows] = p1;
+            const int64_t p = p1 - p0;
             k[i] = (int32_t)min(p, (int64_t)INT32_MAX);
             prod[r] = k[i];
             b[i] = bin_of(spec, k[i], k[i], -2, ent2_of(spec, A, r));
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(BIN_BLOCK) void k_an_rows(const int64_t *poff, int6
         for (int i = 0; i < BIN_BLOCK / WAVE; ++i) mx = max(mx, wmx[i]);
         if (mx > 0) atomicMax(&cnt->max_prod, mx);
         if (blockIdx.x == 0) {
-            cnt->flops = (unsigned long long)(poff[rows] - poff[0]);
+            cnt->flops = (unsigned long long)(axp[n_entries] - axp[row_q(A, 0, n_entries, cnt)]);
             cnt->a_base = (long long)A.base();
         }
     }
@@ -658,6 +679,254 @@ __global__ __launch_bounds__(256) void k_dup_place(const RowRef *list, int32_t c
         const uint2 e = pr[i];
         const uint32_t rk = pref[e.x >> 5] + (uint32_t)__popc(bits[e.x >> 5] & ((1u << (e.x & 31)) - 1u));
         dt[e.x - rk] = (int32_t)e.y;
+    }
+}
+
+// Column-bitmap symbolic of the partitioned rows (> SYM2_MAX products) when
+// B's columns fit one LDS bitmap (ncw words, n_cols <= 32 * CBM_MAXW): one
+// 1024-lane workgroup per row, no partitions, no bucket pass.
+//  1. every product sets its column's bit: the products that find it clear
+//     are the row's distinct columns (nnz = products - the others); the
+//     others (duplicates) list their column;
+//  2. the bitmap is rebuilt from the list: the columns with more than one
+//     product, ranked by a superblock popcount prefix;
+//  3. the products of those columns take the smallest product index per
+//     column (atomicMin on a compact table in the row's work space): the
+//     first touch, as the sequential loop of CSR_MUL_CSR finds it
+//     (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:133-189);
+//  4. first-touch bitmap = every product but the duplicates, its word
+//     prefixes, and the duplicates' first touches at their product-order
+//     index when the row's list holds them (else dupn = -1: table path).
+// Outputs are those of k_symbolic_part + k_bitmap_prefix + k_dup_place.
+constexpr int CBM_BLOCK = 1024;
+constexpr int CBM_SB = 8;            // bitmap words per rank superblock
+constexpr int32_t CBM_MAXW = 36096;  // 4.5 B per word of LDS (bitmap + superblock prefix)
+// 1: the duplicate pass walks a list of the multi columns' products made by
+// the first-touch pass (when it fits the row's work space), 0: a third sweep
+constexpr int CBM_LIST = 1;
+__host__ __device__ constexpr int32_t cbm_words(int64_t cols) {
+    return (int32_t)(((cols + 31) / 32 + CBM_SB - 1) / CBM_SB * CBM_SB);
+}
+__host__ __device__ constexpr size_t cbm_lds_bytes(int32_t ncw) { return 4ull * ncw + 4ull * (ncw / CBM_SB); }
+static_assert(cbm_lds_bytes(CBM_MAXW) + 512 <= 160 * 1024, "column bitmap beyond the LDS");
+
+struct CbmArgs {
+    const int32_t *tcol;   // the rows' product columns (k_expand_part, every row)
+    const RowRef *list;   // ref.q0: the row's work space (2 words per product), ref.n: products
+    int32_t ncw;
+    uint2 *work;
+    Bitmap bm;
+    int32_t *nnz_row;
+    const int64_t *dup_off;
+    int32_t *dupn, *gdupt;
+    int32_t div, dmax;
+};
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t cbm[];
+    __shared__ int scratch[64];
+    __shared__ int ncnt[3];
+    const int NCW = a.ncw;
+    uint32_t *spre = cbm + NCW;
+    const RowRef ref = a.list[blockIdx.x];
+    const int32_t row = ref.row;
+    const int32_t P = ref.n;
+    const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t *wk = (uint32_t *)(a.work + ref.q0);   // 2 P words
+    for (int i = tid; i < NCW / 4; i += CBM_BLOCK) ((uint4 *)cbm)[i] = make_uint4(0u, 0u, 0u, 0u);
+    if (tid < 3) ncnt[tid] = 0;
+    __syncthreads();
+    // the row's product columns from its expansion (k_expand_part): flat,
+    // coalesced, U per lane in flight; lanes hold consecutive products
+    constexpr int U = 4;
+    const int32_t *tc = a.tcol + ref.q0;
+    auto sweep = [&](auto &&visit) {
+        for (int32_t b0 = 0; b0 < P; b0 += U * CBM_BLOCK) {
+            int32_t c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t p = b0 + u * CBM_BLOCK + tid;
+                c[u] = p < P ? tc[p] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int32_t p = b0 + u * CBM_BLOCK + tid;
+                visit(p < P, c[u], p);
+            }
+        }
+    };
+    // wave-aggregated slot of an LDS counter
+    auto slot = [&](bool on, int k) -> int {
+        const uint64_t m = __ballot(on);
+        int at = 0;
+        if (m) {
+            if (lane == 0) at = atomicAdd(&ncnt[k], (int)__popcll(m));
+            at = __shfl(at, 0) + (int)__popcll(m & lt);
+        }
+        return at;
+    };
+    // ---- 1. distinct columns; the duplicates list their column
+    sweep([&](bool act, int32_t c, int32_t) {
+        const uint32_t bit = 1u << (c & 31);
+        uint32_t old = 0u;
+        if (act) old = atomicOr(&cbm[c >> 5], bit);
+        const bool dup = act && (old & bit);
+        const int at = slot(dup, 0);
+        if (dup) wk[at] = (uint32_t)c;
+    });
+    __syncthreads();
+    const int32_t nd = ncnt[0];
+    const int32_t nnz = P - nd;
+    const int32_t W = (P + 31) >> 5;
+    uint32_t *gbits = a.bm.bits + a.bm.off[row];
+    uint32_t *gpref = a.bm.pref + a.bm.off[row];
+    const int32_t cap = a.div > 0 ? min(P / a.div, a.dmax) : 0;
+    const bool keep = nd <= cap;
+    int M = 0;   // columns of more than one product
+    uint2 *pairs = nullptr;   // the duplicates (product, first touch) when kept
+    // first-touch words: every product until the duplicates clear theirs
+    for (int32_t i = tid; i < W; i += CBM_BLOCK)
+        gbits[i] = (i < W - 1 || (P & 31) == 0) ? ~0u : ((1u << (P & 31)) - 1u);
+    if (nd > 0) {
+        // ---- 2. columns of more than one product + their ranks
+        for (int i = tid; i < NCW / 4; i += CBM_BLOCK) ((uint4 *)cbm)[i] = make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        for (int32_t i = tid; i < nd; i += CBM_BLOCK) {
+            const uint32_t c = wk[i];
+            atomicOr(&cbm[c >> 5], 1u << (c & 31));
+        }
+        __syncthreads();
+        const int nsb = NCW / CBM_SB;
+        constexpr int SPT = (CBM_MAXW / CBM_SB + CBM_BLOCK - 1) / CBM_BLOCK;   // superblocks per thread
+        int v[SPT], sum = 0;
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+            const int sb = tid * SPT + k;
+            v[k] = 0;
+            if (sb < nsb) {
+                const uint4 x = ((const uint4 *)cbm)[2 * sb], y = ((const uint4 *)cbm)[2 * sb + 1];
+                v[k] = __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w) + __popc(y.x) + __popc(y.y) +
+                       __popc(y.z) + __popc(y.w);
+            }
+            sum += v[k];
+        }
+        int run = Team<CBM_BLOCK>::excl_sum(sum, M, scratch);
+#pragma unroll
+        for (int k = 0; k < SPT; ++k) {
+            const int sb = tid * SPT + k;
+            if (sb < nsb) spre[sb] = (uint32_t)run;
+            run += v[k];
+        }
+        // own[0, M): the smallest product per multi column (the list is dead)
+        uint32_t *own = wk;
+        for (int32_t i = tid; i < M; i += CBM_BLOCK) own[i] = 0x7fffffffu;
+        __threadfence();
+        __syncthreads();
+        auto multi = [&](int32_t c) -> bool { return (cbm[c >> 5] >> (c & 31)) & 1u; };
+        auto rank = [&](int32_t c) -> uint32_t {
+            const int wi = c >> 5, sb = c >> 8;
+            uint32_t r = spre[sb] + (uint32_t)__popc(cbm[wi] & ((1u << (c & 31)) - 1u));
+            for (int j = sb * CBM_SB; j < wi; ++j) r += (uint32_t)__popc(cbm[j]);
+            return r;
+        };
+        // ---- 3. first touch of each multi column (products in order: a
+        // product above the column's current minimum issues no atomic, so a
+        // hub column's later products do not queue on one L2 address); the
+        // multi columns' products are listed (p, rank) when the list fits
+        const int32_t m0 = (M + 1) & ~1;
+        const int32_t mcap = CBM_LIST ? (2 * P - m0) / 2 : 0;
+        uint2 *ml = (uint2 *)(wk + m0);
+        sweep([&](bool act, int32_t c, int32_t p) {
+            const bool on = act && multi(c);
+            uint32_t r = 0u;
+            if (on) {
+                r = rank(c);
+                uint32_t *o = &own[r];
+                if (ld_agent(o) > (uint32_t)p) atomicMin(o, (uint32_t)p);
+            }
+            if (CBM_LIST) {
+                const int at = slot(on, 2);
+                if (on && at < mcap) ml[at] = make_uint2((uint32_t)p, r);
+            }
+        });
+        __threadfence();
+        __syncthreads();
+        // ---- 4. duplicates: clear their bits, list (product, first touch)
+        const int32_t nml = CBM_LIST ? ncnt[2] : 0;
+        const bool listed = CBM_LIST && nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
+        pairs = (uint2 *)(wk + (listed ? m0 + 2 * nml : m0));
+        if (listed) {
+            for (int32_t i0 = 0; i0 < nml; i0 += CBM_BLOCK) {
+                const int32_t i = i0 + tid;
+                uint2 e = make_uint2(0u, 0u);
+                uint32_t f = 0u;
+                bool dup = false;
+                if (i < nml) {
+                    e = ml[i];
+                    f = ld_agent(&own[e.y]);
+                    dup = f != e.x;
+                }
+                if (dup) atomicAnd(&gbits[e.x >> 5], ~(1u << (e.x & 31)));
+                if (keep) {
+                    const int at = slot(dup, 1);
+                    if (dup) pairs[at] = make_uint2(e.x, f);
+                }
+            }
+        } else {
+            sweep([&](bool act, int32_t c, int32_t p) {
+                uint32_t f = 0u;
+                bool dup = false;
+                if (act && multi(c)) {
+                    f = ld_agent(&own[rank(c)]);
+                    dup = f != (uint32_t)p;
+                }
+                // the lanes' products are consecutive: one atomic per bitmap word
+                const uint64_t dm = __ballot(dup);
+                if (dup) {
+                    const int32_t pb = p - lane, wi = p >> 5;
+                    const int lo = max(0, wi * 32 - pb), hi = min(WAVE - 1, wi * 32 + 31 - pb);
+                    const uint64_t mine = dm & (((1ull << (hi - lo + 1)) - 1ull) << lo);
+                    if (lane == __builtin_ctzll(mine))
+                        atomicAnd(&gbits[wi], ~((uint32_t)(mine >> lo) << ((pb + lo) & 31)));
+                }
+                if (keep) {
+                    const int at = slot(dup, 1);
+                    if (dup) pairs[at] = make_uint2((uint32_t)p, f);
+                }
+            });
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    // ---- word prefixes (tiles of CBM_BLOCK words, carried)
+    int carry = 0;
+    for (int32_t w0 = 0; w0 < W; w0 += CBM_BLOCK) {
+        const int32_t i = w0 + tid;
+        const int cnt = i < W ? __popc(ld_agent(&gbits[i])) : 0;
+        int tot;
+        const int ex = Team<CBM_BLOCK>::excl_sum(cnt, tot, scratch);
+        if (i < W) gpref[i] = (uint32_t)(carry + ex);
+        carry += tot;
+    }
+    if (nd > 0 && keep) {   // duplicates at their product-order index d = p - rank(p)
+        __threadfence();
+        __syncthreads();
+        int32_t *dt = a.gdupt + a.dup_off[row];
+        for (int32_t i = tid; i < nd; i += CBM_BLOCK) {
+            const uint2 e = pairs[i];
+            const uint32_t wi = e.x >> 5;
+            const uint32_t rk = ld_agent(&gpref[wi]) + (uint32_t)__popc(ld_agent(&gbits[wi]) & ((1u << (e.x & 31)) - 1u));
+            dt[e.x - rk] = (int32_t)e.y;
+        }
+    }
+    if (tid == 0) {
+        a.nnz_row[row] = nnz;
+        a.dupn[row] = keep ? nd : -1;
     }
 }
 
@@ -1398,7 +1667,8 @@ __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const in
                                                      const RowRef *list, const int32_t *bcol, int32_t *tcol,
                                                      int32_t part_cap) {
     const RowRef ref = list[blockIdx.x];
-    if (nparts_of(ref.n, part_cap) <= (uint32_t)PB_MAXP) return;   // bucketed from B instead
+    // part_cap 0: every row (k_sym_cbm); else the rows beyond PB_MAXP partitions
+    if (part_cap > 0 && nparts_of(ref.n, part_cap) <= (uint32_t)PB_MAXP) return;   // bucketed from B instead
     int64_t s;
     int32_t n;
     A.row(ref.row, s, n);
@@ -1456,6 +1726,16 @@ constexpr int SYM_PART_LOG2S = 14; // table slots of a symbolic partition (2^14 
 constexpr int32_t SYM_PART_CAP = ((1 << SYM_PART_LOG2S) * 2) / 3;   // products per symbolic partition
 constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
+// serial ns per product of the column-bitmap symbolic (stream balancing)
+constexpr double CBM_COST = 12.0;
+// IAS_SYM_CBM=0: the partitioned rows take the hash partitions (A/B)
+static bool cbm_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SYM_CBM");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 
 // LDS bins: upper bound of the key and kernel configuration; table slots
 // S = ceil(1.5 * upper).
@@ -1515,11 +1795,26 @@ static constexpr bool val_bins_covered() {
 }
 static_assert(val_bins_covered(), "value-bin emission does not cover a bin's table");
 
-static BinSpec sym_spec() {
+// Symbolic LDS bins in use: all of SYM2_BINS, or, when the column-bitmap
+// symbolic applies, those below IAS_SYM_CBM_MIN products (the longer rows
+// join the partitioned bin: k_sym_cbm).
+static int sym_nval(bool cbm) {
+    static const int nv = [] {
+        const char *e = getenv("IAS_SYM_CBM_MIN");
+        if (!e || !*e) return N_SYM2;
+        const long v = atol(e);
+        int n = 0;
+        while (n < N_SYM2 && SYM2_BINS[n].upper < v) ++n;
+        return n;
+    }();
+    return cbm ? nv : N_SYM2;
+}
+
+static BinSpec sym_spec(int nval = N_SYM2) {
     BinSpec s{};
     s.ndw = 0;
-    s.nval = N_SYM2;
-    for (int i = 0; i < N_SYM2; ++i) {
+    s.nval = nval;
+    for (int i = 0; i < nval; ++i) {
         s.upper[i + 1] = SYM2_BINS[i].upper;
         s.dcap[i + 1] = dcap_for(SYM2_BINS[i].upper);
     }
@@ -1953,7 +2248,8 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     HIPC(hipSetDevice(device));
     n_rows = rows;
     n_entries = a_entries;
-    const BinSpec ss = sym_spec();
+    cbm_path = cbm_words(n_cols) <= CBM_MAXW && cbm_enabled();
+    const BinSpec ss = sym_spec(sym_nval(cbm_path));
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
@@ -1992,9 +2288,10 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     } else {
         HIPC(hipMemsetAsync(axp, 0, sizeof(int64_t), s));
     }
-    k_row_poff<<<grid_for(rows + 1, 256), 256, 0, s>>>(A, rows, axp, a_entries, poff, dc);
     if (rows > 0)
-        BIN_LAUNCH(k_an_rows, rows, s, poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
+        BIN_LAUNCH(k_an_rows, rows, s, axp, a_entries, poff, rows, as<int32_t>(bufs[B_PROD]), ss, dc, A);
+    else
+        k_row_poff<<<1, 64, 0, s>>>(A, rows, axp, a_entries, poff, dc);
     CHECK_LAUNCH("product offsets", s);
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
@@ -2005,7 +2302,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     n_cols = cols;
     IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
-    const BinSpec ss = sym_spec(), ns = num_spec();
+    const BinSpec ss = sym_spec(sym_nval(cbm_path)), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
     Counters *hc = (Counters *)host_counters;
@@ -2027,6 +2324,10 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
 
     // ---- expansion of the partitioned rows' product columns (in their
     // compact space; the other bins gather from B)
+    // the partitioned rows: one LDS column bitmap per row when B's columns
+    // fit it (k_sym_cbm), else hash partitions (expansion + buckets)
+    const int32_t ncw = cbm_words(cols);
+    const bool cbm = cbm_path;
     IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>((int64_t)c1.part_prod, 1)));
     const int32_t *tcol = as<int32_t>(bufs[B_TCOL]);
 
@@ -2046,7 +2347,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_DUPP, sizeof(uint2) * (c1.dup_slots + 1)));
     Bitmap bm{as<uint32_t>(bufs[B_BITS]), as<uint32_t>(bufs[B_BPREF]), as<int64_t>(bufs[B_BMOFF])};
     const StArgs sa{bm, as<int64_t>(bufs[B_DUPOFF]), as<int32_t>(bufs[B_DUPN]), as<int32_t>(bufs[B_DUPT])};
-    if (c1.count[sym_part] > 0) HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
+    if (c1.count[sym_part] > 0 && !cbm) HIPC(hipMemsetAsync(bm.bits, 0, sizeof(uint32_t) * c1.bm_words, s));
     RowRef *SL = as<RowRef>(bufs[B_SLIST]);
     int32_t *nnz = as<int32_t>(bufs[B_NNZ]);
     if (rows > 0)
@@ -2071,7 +2372,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     {
         double load[NSIDE] = {};
         std::vector<std::pair<double, int>> jobs;
-        if (c1.count[sym_part] > 0) jobs.push_back({40.0 * (double)c1.part_prod, sym_part});
+        if (c1.count[sym_part] > 0) jobs.push_back({(cbm ? CBM_COST : 40.0) * (double)c1.part_prod, sym_part});
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
                 const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
@@ -2087,18 +2388,30 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     }
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
-        k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
-                                                               as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
-        k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
-                                                 as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
-                                                 as<PartSpan>(bufs[B_PSPAN]));
-        k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
-            tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-            PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]));
-        k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
-        k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
-                                      sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
-        CHECK_LAUNCH("k_symbolic_part", t);
+        if (cbm) {
+            static bool cbm_done = false;
+            const size_t lds = cbm_lds_bytes(ncw);
+            allow_lds(k_sym_cbm, cbm_done, lds);
+            k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+                                                               as<int32_t>(bufs[B_TCOL]), 0);
+            const CbmArgs ca{tcol, SL + st[sym_part], ncw, as<uint2>(bufs[B_PBKT]), bm, nnz,
+                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP};
+            k_sym_cbm<<<c, CBM_BLOCK, lds, t>>>(ca);
+            CHECK_LAUNCH("k_sym_cbm", t);
+        } else {
+            k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+                                                                   as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);
+            k_part_bucket<<<c, PB_BLOCK, 0, t>>>(A, ax, axp, poff, B.col, SL + st[sym_part], c, as<int64_t>(bufs[B_PFIRST]),
+                                                     as<int64_t>(bufs[B_PBOFF]), SYM_PART_CAP, as<uint2>(bufs[B_PBKT]),
+                                                     as<PartSpan>(bufs[B_PSPAN]));
+            k_symbolic_part<1024, 12, SYM_PART_LOG2S><<<(unsigned)c1.items, 1024, 0, t>>>(
+                tcol, as<PartItem>(bufs[B_SITEM]), bm, nnz, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
+                PART_DCAP_DIV, FIXBIG_CAP, &dc2->overflow, as<uint2>(bufs[B_PBKT]), as<PartSpan>(bufs[B_PSPAN]));
+            k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+            k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
+                                          sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
+            CHECK_LAUNCH("k_symbolic_part", t);
+        }
     }
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {

@@ -100,6 +100,7 @@ struct ias_plan {
     // state carried from symbolic() to numeric() (and the row sort)
     int64_t n_rows = 0;
     int64_t n_cols = 0;      // C's columns
+    bool cbm_path = false;   // partitioned rows: one LDS column bitmap per row (k_sym_cbm)
     int64_t n_entries = 0;   // stored entries of A (expanded-A length)
     int64_t nnz_total = 0;
     int64_t flops = 0;

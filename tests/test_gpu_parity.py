@@ -227,6 +227,17 @@ def test_csr_duplicate_tiers():
     np.testing.assert_array_equal(bits(got_v), bits(refc.val))
 
 
+def test_csr_duplicate_tiers_hash_partitions():
+    """The same tiers with B declared 1.2M columns wide: beyond one LDS column
+    bitmap (k_sym_cbm), so the partitioned rows take the hash partitions."""
+    A, B = duplicate_tiers()
+    B = ias.HostCsr(B.rows, 1_200_000, B.row_ptr, B.col, B.val)
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    got, rep = ias.spgemm(A, B)
+    assert rep.max_row_products == 30000
+    assert_csr_identical(got, ref, "duplicate tiers, hash partitions")
+
+
 def wide_row(n=1 << 20, head=1000, per=600):
     """Row 0 reaches head*per = 600k distinct columns: beyond the 19-bit rank
     field of the LDS/partition tables, so the 64-bit global-table path runs."""
