@@ -586,7 +586,7 @@ static ias_status dia_mul(const ias_dia *A, const ias_dia *B, ias_dia *C, const 
     }
     HIPC(hipGetLastError());
     if (e1) HIPC(hipEventRecord(e1, s));
-    HIPC(hipStreamSynchronize(s));
+    HIPC((hipError_t)host_wait(s));
     if (rep) {
         float t = 0;
         if (e0 && e1) hipEventElapsedTime(&t, e0, e1);

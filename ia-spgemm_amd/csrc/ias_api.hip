@@ -877,7 +877,7 @@ extern "C" ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, cons
     if (row_ptr_c) {
         HIPC(hipMemcpyAsync(row_ptr_c, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
                             hipMemcpyDeviceToDevice, (hipStream_t)plan->stream));
-        HIPC(hipStreamSynchronize((hipStream_t)plan->stream));
+        HIPC((hipError_t)host_wait(plan->stream));
     }
     return IAS_SUCCESS;
 }
@@ -908,7 +908,7 @@ extern "C" ias_status ias_csr_mul_csr_compute(ias_plan *plan, const ias_csr *A, 
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, plan->max_nnz));
     // C is complete when this returns (callers may read or free it at once,
     // from any stream), as the reference's timer sync does (GPU/detail/utime.h).
-    HIPC(hipStreamSynchronize(s));
+    HIPC((hipError_t)host_wait(s));
     return IAS_SUCCESS;
 }
 
@@ -947,8 +947,23 @@ extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, con
     C->nnz = nnz;
     if (order == IAS_ORDER_SORTED)
         IAS_TRY(ias_sort_rows_device(plan, C->row_ptr, A->rows, C->col, C->val, 0));
-    HIPC(hipStreamSynchronize(s));
+    HIPC((hipError_t)host_wait(s));
     return IAS_SUCCESS;
+}
+
+int ias::host_wait(void *stream) {
+    static const long spin_us = [] {
+        const char *e = getenv("IAS_SPIN_US");
+        return e && *e ? atol(e) : 200L;
+    }();
+    hipStream_t s = (hipStream_t)stream;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return (int)e;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
+            return (int)hipStreamSynchronize(s);
+    }
 }
 
 // =================================================================== helpers

@@ -26,6 +26,12 @@ ias_status dev_memset(void *p, int value, size_t bytes, int device);
 // returns the bytes released.
 size_t release_device_memory(int device, const ias_plan *keep);
 
+// Host wait for a stream's work (returns a hipError_t): polls for up to
+// IAS_SPIN_US microseconds (default 200), then blocks.  A blocking wait wakes
+// the host tens of µs after the GPU finishes, which small products (K1: a
+// few tens of µs per kernel, two host reads per call) would pay per wait.
+int host_wait(void *stream);
+
 // Record the last HIP/internal error message for ias_status_string's detail.
 void set_last_error(const char *fmt, ...);
 

@@ -691,19 +691,20 @@ __global__ __launch_bounds__(256) void k_dup_place(const RowRef *list, int32_t c
 //  2. the bitmap is rebuilt from the list: the columns with more than one
 //     product, ranked by a superblock popcount prefix;
 //  3. the products of those columns take the smallest product index per
-//     column (atomicMin on a compact table in the row's work space): the
+//     column (atomicMin on a compact table indexed by rank: in the LDS left
+//     beyond the bitmap when it fits, else in the row's work space): the
 //     first touch, as the sequential loop of CSR_MUL_CSR finds it
-//     (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:133-189);
-//  4. first-touch bitmap = every product but the duplicates, its word
-//     prefixes, and the duplicates' first touches at their product-order
-//     index when the row's list holds them (else dupn = -1: table path).
+//     (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:133-189), and are
+//     listed (product, rank);
+//  4. first-touch bitmap = every product but the duplicates (built in the
+//     LDS over the dead column bitmap when it fits), its word prefixes, and
+//     the duplicates' first touches at their product-order index when the
+//     row's list holds them (else dupn = -1: table path).
 // Outputs are those of k_symbolic_part + k_bitmap_prefix + k_dup_place.
 constexpr int CBM_BLOCK = 1024;
 constexpr int CBM_SB = 8;            // bitmap words per rank superblock
 constexpr int32_t CBM_MAXW = 36096;  // 4.5 B per word of LDS (bitmap + superblock prefix)
-// 1: the duplicate pass walks a list of the multi columns' products made by
-// the first-touch pass (when it fits the row's work space), 0: a third sweep
-constexpr int CBM_LIST = 1;
+constexpr int CBM_U = 8;             // product columns per lane per block of a sweep
 __host__ __device__ constexpr int32_t cbm_words(int64_t cols) {
     return (int32_t)(((cols + 31) / 32 + CBM_SB - 1) / CBM_SB * CBM_SB);
 }
@@ -720,8 +721,13 @@ struct CbmArgs {
     const int64_t *dup_off;
     int32_t *dupn, *gdupt;
     int32_t div, dmax;
+    int32_t own_cap;   // LDS words beyond the bitmap + prefixes (the minima table when it fits)
 };
 
+// Workgroup-only sharing in k_sym_cbm: plain stores and loads meet in the
+// CU's L1 after a barrier; values changed by global atomics (performed in
+// L2) are read past the L1 with this load.  No device-scope fence: on gfx950
+// one writes back and invalidates the XCD's L2.
 __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -742,22 +748,34 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     if (tid < 3) ncnt[tid] = 0;
     __syncthreads();
     // the row's product columns from its expansion (k_expand_part): flat,
-    // coalesced, U per lane in flight; lanes hold consecutive products
-    constexpr int U = 4;
+    // coalesced, lanes on consecutive products; blocks of U per lane, the
+    // next block's loads issued before this block's work (2U in flight)
+    constexpr int U = CBM_U;
     const int32_t *tc = a.tcol + ref.q0;
-    auto sweep = [&](auto &&visit) {
-        for (int32_t b0 = 0; b0 < P; b0 += U * CBM_BLOCK) {
-            int32_t c[U];
+    auto load = [&](int32_t b0, int32_t(&c)[U]) {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t p = b0 + u * CBM_BLOCK + tid;
-                c[u] = p < P ? tc[p] : 0;
-            }
+        for (int u = 0; u < U; ++u) {
+            const int32_t p = b0 + u * CBM_BLOCK + tid;
+            c[u] = p < P ? tc[p] : 0;
+        }
+    };
+    auto sweep = [&](auto &&visit) {
+        int32_t ca[U], cb[U];
+        auto work = [&](int32_t b0, const int32_t(&c)[U]) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int32_t p = b0 + u * CBM_BLOCK + tid;
                 visit(p < P, c[u], p);
             }
+        };
+        constexpr int32_t STEP = U * CBM_BLOCK;
+        load(0, ca);
+        for (int32_t b0 = 0; b0 < P; b0 += 2 * STEP) {
+            if (b0 + STEP < P) load(b0 + STEP, cb);
+            work(b0, ca);
+            if (b0 + STEP >= P) break;
+            if (b0 + 2 * STEP < P) load(b0 + 2 * STEP, ca);
+            work(b0 + STEP, cb);
         }
     };
     // wave-aggregated slot of an LDS counter
@@ -789,9 +807,10 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     const bool keep = nd <= cap;
     int M = 0;   // columns of more than one product
     uint2 *pairs = nullptr;   // the duplicates (product, first touch) when kept
-    // first-touch words: every product until the duplicates clear theirs
-    for (int32_t i = tid; i < W; i += CBM_BLOCK)
-        gbits[i] = (i < W - 1 || (P & 31) == 0) ? ~0u : ((1u << (P & 31)) - 1u);
+    bool lwords = false;      // first-touch words in LDS (over the dead column bitmap)
+    auto full_word = [&](int32_t i) -> uint32_t {
+        return (i < W - 1 || (P & 31) == 0) ? ~0u : ((1u << (P & 31)) - 1u);
+    };
     if (nd > 0) {
         // ---- 2. columns of more than one product + their ranks
         for (int i = tid; i < NCW / 4; i += CBM_BLOCK) ((uint4 *)cbm)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -822,10 +841,11 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             if (sb < nsb) spre[sb] = (uint32_t)run;
             run += v[k];
         }
-        // own[0, M): the smallest product per multi column (the list is dead)
-        uint32_t *own = wk;
+        // own[0, M): the smallest product per multi column — in the LDS beyond
+        // the bitmap when it fits, else over the (dead) list in the work space
+        const bool own_l = M <= a.own_cap;
+        uint32_t *own = own_l ? spre + nsb : wk;
         for (int32_t i = tid; i < M; i += CBM_BLOCK) own[i] = 0x7fffffffu;
-        __threadfence();
         __syncthreads();
         auto multi = [&](int32_t c) -> bool { return (cbm[c >> 5] >> (c & 31)) & 1u; };
         auto rank = [&](int32_t c) -> uint32_t {
@@ -834,32 +854,41 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             for (int j = sb * CBM_SB; j < wi; ++j) r += (uint32_t)__popc(cbm[j]);
             return r;
         };
-        // ---- 3. first touch of each multi column (products in order: a
-        // product above the column's current minimum issues no atomic, so a
-        // hub column's later products do not queue on one L2 address); the
-        // multi columns' products are listed (p, rank) when the list fits
-        const int32_t m0 = (M + 1) & ~1;
-        const int32_t mcap = CBM_LIST ? (2 * P - m0) / 2 : 0;
+        // ---- 3. first touch of each multi column; its products listed (p,
+        // rank) when the list fits the work space.  Global own: products in
+        // order, one above the column's current minimum issues no atomic (a
+        // hub column's later products do not queue on one L2 address).
+        const int32_t m0 = own_l ? 0 : (M + 1) & ~1;
+        const int32_t mcap = (2 * P - m0) / 2;
         uint2 *ml = (uint2 *)(wk + m0);
         sweep([&](bool act, int32_t c, int32_t p) {
             const bool on = act && multi(c);
             uint32_t r = 0u;
             if (on) {
                 r = rank(c);
-                uint32_t *o = &own[r];
-                if (ld_agent(o) > (uint32_t)p) atomicMin(o, (uint32_t)p);
+                if (own_l) {
+                    atomicMin(&own[r], (uint32_t)p);
+                } else {
+                    uint32_t *o = &own[r];
+                    if (ld_agent(o) > (uint32_t)p) atomicMin(o, (uint32_t)p);
+                }
             }
-            if (CBM_LIST) {
-                const int at = slot(on, 2);
-                if (on && at < mcap) ml[at] = make_uint2((uint32_t)p, r);
-            }
+            const int at = slot(on, 2);
+            if (on && at < mcap) ml[at] = make_uint2((uint32_t)p, r);
         });
-        __threadfence();
         __syncthreads();
-        // ---- 4. duplicates: clear their bits, list (product, first touch)
-        const int32_t nml = CBM_LIST ? ncnt[2] : 0;
-        const bool listed = CBM_LIST && nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
+        // ---- 4. duplicates: clear their first-touch bits, list (product, first touch)
+        const int32_t nml = ncnt[2];
+        const bool listed = nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
         pairs = (uint2 *)(wk + (listed ? m0 + 2 * nml : m0));
+        lwords = listed && W <= NCW;
+        if (lwords) {
+            for (int32_t i = tid; i < W; i += CBM_BLOCK) cbm[i] = full_word(i);
+            __syncthreads();
+        } else {
+            for (int32_t i = tid; i < W; i += CBM_BLOCK) gbits[i] = full_word(i);
+            __syncthreads();
+        }
         if (listed) {
             for (int32_t i0 = 0; i0 < nml; i0 += CBM_BLOCK) {
                 const int32_t i = i0 + tid;
@@ -868,10 +897,14 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
                 bool dup = false;
                 if (i < nml) {
                     e = ml[i];
-                    f = ld_agent(&own[e.y]);
+                    f = own_l ? own[e.y] : ld_agent(&own[e.y]);
                     dup = f != e.x;
                 }
-                if (dup) atomicAnd(&gbits[e.x >> 5], ~(1u << (e.x & 31)));
+                if (dup) {
+                    const uint32_t m = ~(1u << (e.x & 31));
+                    if (lwords) atomicAnd(&cbm[e.x >> 5], m);
+                    else atomicAnd(&gbits[e.x >> 5], m);
+                }
                 if (keep) {
                     const int at = slot(dup, 1);
                     if (dup) pairs[at] = make_uint2(e.x, f);
@@ -882,7 +915,8 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
                 uint32_t f = 0u;
                 bool dup = false;
                 if (act && multi(c)) {
-                    f = ld_agent(&own[rank(c)]);
+                    const uint32_t r = rank(c);
+                    f = own_l ? own[r] : ld_agent(&own[r]);
                     dup = f != (uint32_t)p;
                 }
                 // the lanes' products are consecutive: one atomic per bitmap word
@@ -901,26 +935,31 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             });
         }
     }
-    __threadfence();
     __syncthreads();
-    // ---- word prefixes (tiles of CBM_BLOCK words, carried)
+    // ---- words (from the LDS, or all ones without duplicates) and their
+    // prefixes, tiles of CBM_BLOCK words, carried
+    auto word = [&](int32_t i) -> uint32_t {
+        return nd == 0 ? full_word(i) : (lwords ? cbm[i] : ld_agent(&gbits[i]));
+    };
     int carry = 0;
     for (int32_t w0 = 0; w0 < W; w0 += CBM_BLOCK) {
         const int32_t i = w0 + tid;
-        const int cnt = i < W ? __popc(ld_agent(&gbits[i])) : 0;
+        const uint32_t wv = i < W ? word(i) : 0u;
         int tot;
-        const int ex = Team<CBM_BLOCK>::excl_sum(cnt, tot, scratch);
-        if (i < W) gpref[i] = (uint32_t)(carry + ex);
+        const int ex = Team<CBM_BLOCK>::excl_sum(__popc(wv), tot, scratch);
+        if (i < W) {
+            gpref[i] = (uint32_t)(carry + ex);
+            if (nd == 0 || lwords) gbits[i] = wv;
+        }
         carry += tot;
     }
     if (nd > 0 && keep) {   // duplicates at their product-order index d = p - rank(p)
-        __threadfence();
         __syncthreads();
         int32_t *dt = a.gdupt + a.dup_off[row];
         for (int32_t i = tid; i < nd; i += CBM_BLOCK) {
             const uint2 e = pairs[i];
             const uint32_t wi = e.x >> 5;
-            const uint32_t rk = ld_agent(&gpref[wi]) + (uint32_t)__popc(ld_agent(&gbits[wi]) & ((1u << (e.x & 31)) - 1u));
+            const uint32_t rk = gpref[wi] + (uint32_t)__popc(word((int32_t)wi) & ((1u << (e.x & 31)) - 1u));
             dt[e.x - rk] = (int32_t)e.y;
         }
     }
@@ -1667,8 +1706,7 @@ __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const in
                                                      const RowRef *list, const int32_t *bcol, int32_t *tcol,
                                                      int32_t part_cap) {
     const RowRef ref = list[blockIdx.x];
-    // part_cap 0: every row (k_sym_cbm); else the rows beyond PB_MAXP partitions
-    if (part_cap > 0 && nparts_of(ref.n, part_cap) <= (uint32_t)PB_MAXP) return;   // bucketed from B instead
+    if (nparts_of(ref.n, part_cap) <= (uint32_t)PB_MAXP) return;   // bucketed from B instead
     int64_t s;
     int32_t n;
     A.row(ref.row, s, n);
@@ -1681,6 +1719,50 @@ __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const in
         const int64_t bs = ax.bstart[q];
         int32_t *dst = tcol + ref.q0 + (axp[q] - p0);
         for (int32_t j = lane; j < bl; j += WAVE) dst[j] = bcol[bs + j];
+    }
+}
+
+// The same expansion for k_sym_cbm, flat over products: a wave takes 64 A
+// entries of the row at a time (lane = entry: B-row start, length; a DPP
+// scan gives each its first product), then walks their products in windows
+// of 64 — product t of the group finds its entry by a 6-step binary search
+// over the lanes' starts — so every gather slot carries a product and each
+// window's stores are one contiguous run (R-MAT's B rows hold ~20 - 30
+// entries: a wave per entry left half its lanes idle).
+__global__ __launch_bounds__(256) void k_expand_flat(Rows A, AxView ax, const int64_t *axp, const int64_t *poff,
+                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol) {
+    const RowRef ref = list[blockIdx.x];
+    int64_t s;
+    int32_t n;
+    A.row(ref.row, s, n);
+    const int64_t q0 = s - A.base();
+    const int64_t p0 = poff[ref.row];
+    const int w = (int)(threadIdx.x / WAVE), lane = (int)(threadIdx.x & (WAVE - 1));
+    const int nw = 4 * (int)gridDim.y;
+    for (int32_t g = ((int32_t)blockIdx.y * 4 + w) * WAVE; g < n; g += nw * WAVE) {
+        const int32_t e = g + lane;
+        int32_t bl = 0;
+        int64_t bs = 0;
+        if (e < n) {
+            bl = ax.blen[q0 + e];
+            bs = ax.bstart[q0 + e];
+        }
+        const int incl = wave_incl_sum(bl);
+        const int excl = incl - bl;
+        const int total = __shfl(incl, WAVE - 1);
+        int32_t *dst = tcol + ref.q0 + (axp[q0 + g] - p0);   // the group's products are contiguous
+        for (int t0 = 0; t0 < total; t0 += WAVE) {
+            const int t = t0 + lane;
+            int j = 0;
+#pragma unroll
+            for (int step = WAVE / 2; step >= 1; step >>= 1) {
+                const int ex = __shfl(excl, j + step);
+                if (ex <= t) j += step;
+            }
+            const int64_t bsj = __shfl(bs, j);
+            const int exj = __shfl(excl, j);
+            if (t < total) dst[t] = bcol[bsj + (t - exj)];
+        }
     }
 }
 
@@ -2310,7 +2392,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     const int64_t *axp = as<int64_t>(bufs[B_AXP]);
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + A's base entry
-    HIPC(hipStreamSynchronize(s));
+    HIPC((hipError_t)host_wait(s));
     const Counters c1 = *hc;
     ax_aval = A.val + (rows > 0 ? c1.a_base : 0);
     const AxView ax = ax_view();
@@ -2390,12 +2472,14 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
         if (cbm) {
             static bool cbm_done = false;
-            const size_t lds = cbm_lds_bytes(ncw);
+            // the minima table takes the LDS left beyond the bitmap (3,968 entries at 2^20 columns)
+            const int32_t own_cap = (int32_t)std::max<int64_t>(0, ((int64_t)160 * 1024 - 512 - (int64_t)cbm_lds_bytes(ncw)) / 4);
+            const size_t lds = cbm_lds_bytes(ncw) + 4ull * own_cap;
             allow_lds(k_sym_cbm, cbm_done, lds);
-            k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
-                                                               as<int32_t>(bufs[B_TCOL]), 0);
+            k_expand_flat<<<dim3((unsigned)c, 4), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+                                                               as<int32_t>(bufs[B_TCOL]));
             const CbmArgs ca{tcol, SL + st[sym_part], ncw, as<uint2>(bufs[B_PBKT]), bm, nnz,
-                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP};
+                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, own_cap};
             k_sym_cbm<<<c, CBM_BLOCK, lds, t>>>(ca);
             CHECK_LAUNCH("k_sym_cbm", t);
         } else {
@@ -2501,7 +2585,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[2], s));
     HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + nnz(C), unit counts
-    HIPC(hipStreamSynchronize(s));
+    HIPC((hipError_t)host_wait(s));
     const Counters c2 = hc[1];
     nnz_total = rows > 0 ? (int64_t)c2.nnz_total : 0;
     n2_units = (int64_t)c2.n2_units;
@@ -2692,7 +2776,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     if (num_count[part_bin] > 0) {
         int32_t of = 0;
         HIPC(hipMemcpyAsync(&of, &dc2->overflow, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-        HIPC(hipStreamSynchronize(s));
+        HIPC((hipError_t)host_wait(s));
         if (of) {
             set_last_error("hash partition table overflow in the numeric pass");
             return IAS_ERROR_OVERFLOW;

@@ -13,13 +13,13 @@ timeout -k 10 300 $T tests/test_gpu_parity.py -m gpu -k "duplicate_tiers or long
    > $OUT/pytest_long.log 2>&1
 rc=$?; tail -2 $OUT/pytest_long.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python tools/nnz_check.py k3p k3 || exit $?
-for m in ${MINS:-8193 4097}; do
+for m in ${MINS-8193 4097}; do
   IAS_SYM_CBM_MIN=$m timeout -k 10 300 python tools/nnz_check.py k3p k3 || exit $?
 done
 B="python bench.py --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor --steps 10 --warmup 3"
 for rep in 1 2; do
   for cfg in k3p k3; do
-    for v in off on ${MINS:-8193 4097} $LIBS; do
+    for v in off on ${MINS-8193 4097} $LIBS; do
       case $v in off) E="IAS_SYM_CBM=0";; on) E="IAS_SYM_CBM=1";; [0-9]*) E="IAS_SYM_CBM_MIN=$v";;
         *) E="IAS_LIB=$PWD/build_var/libias_$v.so";; esac
       env $E timeout -k 10 300 $B --config $cfg > $OUT/${cfg}_${v}_$rep.json 2> $OUT/${cfg}_${v}_$rep.err || exit $?
