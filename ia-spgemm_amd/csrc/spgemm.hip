@@ -19,6 +19,7 @@
 #include <mutex>
 #include <set>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 namespace ias {
@@ -705,6 +706,7 @@ constexpr int CBM_BLOCK = 1024;
 constexpr int CBM_SB = 8;            // bitmap words per rank superblock
 constexpr int32_t CBM_MAXW = 36096;  // 4.5 B per word of LDS (bitmap + superblock prefix)
 constexpr int CBM_U = 8;             // product columns per lane per block of a sweep
+constexpr int CBM_L = 4;             // list items per lane per step of the duplicate pass
 __host__ __device__ constexpr int32_t cbm_words(int64_t cols) {
     return (int32_t)(((cols + 31) / 32 + CBM_SB - 1) / CBM_SB * CBM_SB);
 }
@@ -744,6 +746,8 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1);
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t *wk = (uint32_t *)(a.work + ref.q0);   // 2 P words
+    Timer tmr;   // phases (IAS_TIMING builds): 0 pass 1, 1 multi bitmap, 2 ranks, 3 pass 2, 4 pass 3, 5 prefixes, 6 placement
+    tmr.start();
     for (int i = tid; i < NCW / 4; i += CBM_BLOCK) ((uint4 *)cbm)[i] = make_uint4(0u, 0u, 0u, 0u);
     if (tid < 3) ncnt[tid] = 0;
     __syncthreads();
@@ -759,15 +763,10 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             c[u] = p < P ? tc[p] : 0;
         }
     };
-    auto sweep = [&](auto &&visit) {
+    // blockwise: work(b0, c) gets U columns per lane (products b0 + u *
+    // CBM_BLOCK + tid), so its LDS operations are issued U at a time
+    auto sweep = [&](auto &&work) {
         int32_t ca[U], cb[U];
-        auto work = [&](int32_t b0, const int32_t(&c)[U]) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int32_t p = b0 + u * CBM_BLOCK + tid;
-                visit(p < P, c[u], p);
-            }
-        };
         constexpr int32_t STEP = U * CBM_BLOCK;
         load(0, ca);
         for (int32_t b0 = 0; b0 < P; b0 += 2 * STEP) {
@@ -777,6 +776,26 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             if (b0 + 2 * STEP < P) load(b0 + 2 * STEP, ca);
             work(b0 + STEP, cb);
         }
+    };
+    // wave-aggregated append of up to N items per lane (item j present when
+    // on[j]) to LDS counter k: item j of all lanes takes consecutive slots,
+    // lane order, so each item's stores are one contiguous run (a lane's own
+    // run of slots would scatter every store instruction over 64 lines)
+    auto append = [&](auto const &on, auto &at, int k) {
+        constexpr int N = sizeof(on) / sizeof(on[0]);
+        uint64_t m[N];
+        int tot = 0, off[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            m[j] = __ballot(on[j]);
+            off[j] = tot;
+            tot += (int)__popcll(m[j]);
+        }
+        int base = 0;
+        if (lane == 0 && tot > 0) base = atomicAdd(&ncnt[k], tot);
+        base = __shfl(base, 0);
+#pragma unroll
+        for (int j = 0; j < N; ++j) at[j] = base + off[j] + (int)__popcll(m[j] & lt);
     };
     // wave-aggregated slot of an LDS counter
     auto slot = [&](bool on, int k) -> int {
@@ -789,15 +808,24 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         return at;
     };
     // ---- 1. distinct columns; the duplicates list their column
-    sweep([&](bool act, int32_t c, int32_t) {
-        const uint32_t bit = 1u << (c & 31);
-        uint32_t old = 0u;
-        if (act) old = atomicOr(&cbm[c >> 5], bit);
-        const bool dup = act && (old & bit);
-        const int at = slot(dup, 0);
-        if (dup) wk[at] = (uint32_t)c;
+    sweep([&](int32_t b0, const int32_t(&c)[U]) {
+        uint32_t old[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            old[u] = 0u;
+            if (b0 + u * CBM_BLOCK + tid < P) old[u] = atomicOr(&cbm[c[u] >> 5], 1u << (c[u] & 31));
+        }
+        bool dup[U];
+        int at[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) dup[u] = (old[u] >> (c[u] & 31)) & 1u;
+        append(dup, at, 0);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (dup[u]) wk[at[u]] = (uint32_t)c[u];
     });
     __syncthreads();
+    tmr.mark(0);
     const int32_t nd = ncnt[0];
     const int32_t nnz = P - nd;
     const int32_t W = (P + 31) >> 5;
@@ -820,6 +848,7 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             atomicOr(&cbm[c >> 5], 1u << (c & 31));
         }
         __syncthreads();
+        tmr.mark(1);
         const int nsb = NCW / CBM_SB;
         constexpr int SPT = (CBM_MAXW / CBM_SB + CBM_BLOCK - 1) / CBM_BLOCK;   // superblocks per thread
         int v[SPT], sum = 0;
@@ -843,40 +872,75 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         }
         // own[0, M): the smallest product per multi column — in the LDS beyond
         // the bitmap when it fits, else over the (dead) list in the work space
+        // (two instantiations: a pointer that may be either compiles to flat
+        // instructions, which wait on both the LDS and the memory counters)
         const bool own_l = M <= a.own_cap;
-        uint32_t *own = own_l ? spre + nsb : wk;
-        for (int32_t i = tid; i < M; i += CBM_BLOCK) own[i] = 0x7fffffffu;
-        __syncthreads();
         auto multi = [&](int32_t c) -> bool { return (cbm[c >> 5] >> (c & 31)) & 1u; };
-        auto rank = [&](int32_t c) -> uint32_t {
-            const int wi = c >> 5, sb = c >> 8;
-            uint32_t r = spre[sb] + (uint32_t)__popc(cbm[wi] & ((1u << (c & 31)) - 1u));
-            for (int j = sb * CBM_SB; j < wi; ++j) r += (uint32_t)__popc(cbm[j]);
+        // rank of a multi column from its superblock's 8 words and prefix
+        auto rank_of = [&](int32_t c, const uint4 &x, const uint4 &y, uint32_t sp) -> uint32_t {
+            const int kw = (c >> 5) & (CBM_SB - 1);
+            const uint32_t wv[CBM_SB] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+            uint32_t r = sp;
+#pragma unroll
+            for (int i = 0; i < CBM_SB; ++i)
+                r += (uint32_t)__popc(i < kw ? wv[i] : (i == kw ? wv[i] & ((1u << (c & 31)) - 1u) : 0u));
             return r;
         };
+        auto rank = [&](int32_t c) -> uint32_t {   // three independent LDS reads
+            const int sb = c >> 8;
+            return rank_of(c, ((const uint4 *)cbm)[2 * sb], ((const uint4 *)cbm)[2 * sb + 1], spre[sb]);
+        };
+        auto passes = [&](auto tag) {
+        constexpr bool OL = decltype(tag)::value;
+        uint32_t *own = OL ? spre + nsb : wk;
+        for (int32_t i = tid; i < M; i += CBM_BLOCK) own[i] = 0x7fffffffu;
+        __syncthreads();
+        tmr.mark(2);
         // ---- 3. first touch of each multi column; its products listed (p,
         // rank) when the list fits the work space.  Global own: products in
         // order, one above the column's current minimum issues no atomic (a
         // hub column's later products do not queue on one L2 address).
-        const int32_t m0 = own_l ? 0 : (M + 1) & ~1;
+        const int32_t m0 = OL ? 0 : (M + 1) & ~1;
         const int32_t mcap = (2 * P - m0) / 2;
         uint2 *ml = (uint2 *)(wk + m0);
-        sweep([&](bool act, int32_t c, int32_t p) {
-            const bool on = act && multi(c);
-            uint32_t r = 0u;
-            if (on) {
-                r = rank(c);
-                if (own_l) {
-                    atomicMin(&own[r], (uint32_t)p);
-                } else {
-                    uint32_t *o = &own[r];
-                    if (ld_agent(o) > (uint32_t)p) atomicMin(o, (uint32_t)p);
+        sweep([&](int32_t b0, const int32_t(&c)[U]) {
+            bool on[U];
+            uint32_t r[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) on[u] = b0 + u * CBM_BLOCK + tid < P && multi(c[u]);
+            // ranks of the multi products only: their superblocks' loads
+            // first (masked to those lanes, all in flight), then the sums
+            uint4 x[U], y[U];
+            uint32_t sp[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                x[u] = y[u] = make_uint4(0u, 0u, 0u, 0u);
+                sp[u] = 0u;
+                if (on[u]) {
+                    const int sb = c[u] >> 8;
+                    x[u] = ((const uint4 *)cbm)[2 * sb];
+                    y[u] = ((const uint4 *)cbm)[2 * sb + 1];
+                    sp[u] = spre[sb];
                 }
             }
-            const int at = slot(on, 2);
-            if (on && at < mcap) ml[at] = make_uint2((uint32_t)p, r);
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = rank_of(c[u], x[u], y[u], sp[u]);
+            uint32_t cur[U];   // global own: the current minima, all loads in flight
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = (!OL && on[u]) ? ld_agent(&own[r[u]]) : ~0u;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t p = (uint32_t)(b0 + u * CBM_BLOCK + tid);
+                if (on[u] && cur[u] > p) atomicMin(&own[r[u]], p);
+            }
+            int at[U];
+            append(on, at, 2);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (on[u] && at[u] < mcap) ml[at[u]] = make_uint2((uint32_t)(b0 + u * CBM_BLOCK + tid), r[u]);
         });
         __syncthreads();
+        tmr.mark(3);
         // ---- 4. duplicates: clear their first-touch bits, list (product, first touch)
         const int32_t nml = ncnt[2];
         const bool listed = nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
@@ -889,53 +953,72 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
             for (int32_t i = tid; i < W; i += CBM_BLOCK) gbits[i] = full_word(i);
             __syncthreads();
         }
-        if (listed) {
-            for (int32_t i0 = 0; i0 < nml; i0 += CBM_BLOCK) {
-                const int32_t i = i0 + tid;
-                uint2 e = make_uint2(0u, 0u);
-                uint32_t f = 0u;
-                bool dup = false;
-                if (i < nml) {
-                    e = ml[i];
-                    f = own_l ? own[e.y] : ld_agent(&own[e.y]);
-                    dup = f != e.x;
+        if (listed) {   // CBM_L items per lane per step, each stage's loads in flight together
+            for (int32_t i0 = 0; i0 < nml; i0 += CBM_L * CBM_BLOCK) {
+                uint2 e[CBM_L];
+                uint32_t f[CBM_L];
+#pragma unroll
+                for (int j = 0; j < CBM_L; ++j) {
+                    const int32_t i = i0 + j * CBM_BLOCK + tid;
+                    e[j] = i < nml ? ml[i] : make_uint2(0u, 0u);
                 }
-                if (dup) {
-                    const uint32_t m = ~(1u << (e.x & 31));
-                    if (lwords) atomicAnd(&cbm[e.x >> 5], m);
-                    else atomicAnd(&gbits[e.x >> 5], m);
+#pragma unroll
+                for (int j = 0; j < CBM_L; ++j) {
+                    const bool in = i0 + j * CBM_BLOCK + tid < nml;
+                    f[j] = !in ? 0u : (OL ? own[e[j].y] : ld_agent(&own[e[j].y]));
+                }
+                bool dup[CBM_L];
+#pragma unroll
+                for (int j = 0; j < CBM_L; ++j) {
+                    dup[j] = i0 + j * CBM_BLOCK + tid < nml && f[j] != e[j].x;
+                    if (dup[j]) {
+                        const uint32_t m = ~(1u << (e[j].x & 31));
+                        if (lwords) atomicAnd(&cbm[e[j].x >> 5], m);
+                        else atomicAnd(&gbits[e[j].x >> 5], m);
+                    }
                 }
                 if (keep) {
-                    const int at = slot(dup, 1);
-                    if (dup) pairs[at] = make_uint2(e.x, f);
+                    int at[CBM_L];
+                    append(dup, at, 1);
+#pragma unroll
+                    for (int j = 0; j < CBM_L; ++j)
+                        if (dup[j]) pairs[at[j]] = make_uint2(e[j].x, f[j]);
                 }
             }
         } else {
-            sweep([&](bool act, int32_t c, int32_t p) {
-                uint32_t f = 0u;
-                bool dup = false;
-                if (act && multi(c)) {
-                    const uint32_t r = rank(c);
-                    f = own_l ? own[r] : ld_agent(&own[r]);
-                    dup = f != (uint32_t)p;
-                }
-                // the lanes' products are consecutive: one atomic per bitmap word
-                const uint64_t dm = __ballot(dup);
-                if (dup) {
-                    const int32_t pb = p - lane, wi = p >> 5;
-                    const int lo = max(0, wi * 32 - pb), hi = min(WAVE - 1, wi * 32 + 31 - pb);
-                    const uint64_t mine = dm & (((1ull << (hi - lo + 1)) - 1ull) << lo);
-                    if (lane == __builtin_ctzll(mine))
-                        atomicAnd(&gbits[wi], ~((uint32_t)(mine >> lo) << ((pb + lo) & 31)));
-                }
-                if (keep) {
-                    const int at = slot(dup, 1);
-                    if (dup) pairs[at] = make_uint2((uint32_t)p, f);
+            sweep([&](int32_t b0, const int32_t(&c)[U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int32_t p = b0 + u * CBM_BLOCK + tid;
+                    uint32_t f = 0u;
+                    bool dup = false;
+                    if (p < P && multi(c[u])) {
+                        const uint32_t r = rank(c[u]);
+                        f = OL ? own[r] : ld_agent(&own[r]);
+                        dup = f != (uint32_t)p;
+                    }
+                    // the lanes' products are consecutive: one atomic per bitmap word
+                    const uint64_t dm = __ballot(dup);
+                    if (dup) {
+                        const int32_t pb = p - lane, wi = p >> 5;
+                        const int lo = max(0, wi * 32 - pb), hi = min(WAVE - 1, wi * 32 + 31 - pb);
+                        const uint64_t mine = dm & (((1ull << (hi - lo + 1)) - 1ull) << lo);
+                        if (lane == __builtin_ctzll(mine))
+                            atomicAnd(&gbits[wi], ~((uint32_t)(mine >> lo) << ((pb + lo) & 31)));
+                    }
+                    if (keep) {
+                        const int at = slot(dup, 1);
+                        if (dup) pairs[at] = make_uint2((uint32_t)p, f);
+                    }
                 }
             });
         }
+        };
+        if (own_l) passes(std::true_type{});
+        else passes(std::false_type{});
     }
     __syncthreads();
+    tmr.mark(4);
     // ---- words (from the LDS, or all ones without duplicates) and their
     // prefixes, tiles of CBM_BLOCK words, carried
     auto word = [&](int32_t i) -> uint32_t {
@@ -953,6 +1036,7 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         }
         carry += tot;
     }
+    tmr.mark(5);
     if (nd > 0 && keep) {   // duplicates at their product-order index d = p - rank(p)
         __syncthreads();
         int32_t *dt = a.gdupt + a.dup_off[row];
@@ -967,6 +1051,8 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         a.nnz_row[row] = nnz;
         a.dupn[row] = keep ? nd : -1;
     }
+    tmr.mark(6);
+    tmr.flush(28, tid == 0);   // slot 28: column-bitmap symbolic
 }
 
 // ---------------------------------------------------------------- numeric kernels

@@ -2,7 +2,8 @@
 # k_sym_cbm over the expansion: long-row parity cases, nnz(C) of K3' / K3, then
 # K3' and K3 with the hash partitions (IAS_SYM_CBM=0), the column bitmap for
 # rows beyond 16,384 products, and for rows from IAS_SYM_CBM_MIN = MINS;
-# build_var variants LIBS; serial K3 kernel stats of the default.
+# build_var variants LIBS; serial K3 kernel stats of the default.  SUITE=1:
+# the whole GPU suite after the nnz checks.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,6 +17,10 @@ timeout -k 10 300 python tools/nnz_check.py k3p k3 || exit $?
 for m in ${MINS-8193 4097}; do
   IAS_SYM_CBM_MIN=$m timeout -k 10 300 python tools/nnz_check.py k3p k3 || exit $?
 done
+if [ -n "$SUITE" ]; then
+  timeout -k 10 600 $T tests -m gpu > $OUT/pytest_gpu.log 2>&1
+  rc=$?; tail -2 $OUT/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
+fi
 B="python bench.py --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor --steps 10 --warmup 3"
 for rep in 1 2; do
   for cfg in k3p k3; do

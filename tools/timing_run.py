@@ -8,6 +8,8 @@ Phases (spgemm_kernels.hpp, Timer marks):
     write, 7 duplicate flush
   numeric (k_numeric_st): 0 setup, 1 segment load, 2 gather+write,
     3 segment sync, 4 fix-up barrier, 5 duplicate fix-up
+  sym-cbm (k_sym_cbm): 0 pass 1, 1 multi bitmap, 2 ranks + minima init,
+    3 pass 2, 4 pass 3, 5 word prefixes, 6 placement
 """
 import argparse
 import ctypes as C
@@ -55,6 +57,8 @@ def main():
             kind, team = "sym4", 64
         elif slot == 29:
             kind, team = "sym-part", 1024
+        elif slot == 28:
+            kind, team = "sym-cbm", 1024
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
         print("%-8s TEAM %4d rows %8d  per-row us: %s  sum %.2f" % (
             kind, team, cnt, " ".join("%6.2f" % u for u in us), sum(us)))
