@@ -1894,8 +1894,10 @@ constexpr int SYM_PART_LOG2S = 14; // table slots of a symbolic partition (2^14 
 constexpr int32_t SYM_PART_CAP = ((1 << SYM_PART_LOG2S) * 2) / 3;   // products per symbolic partition
 constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
-// serial ns per product of the column-bitmap symbolic (stream balancing)
-constexpr double CBM_COST = 12.0;
+// serial ns per product of the column-bitmap symbolic with its expansion
+// (stream balancing; K3' 0.55 ms for 27.5 M products; 12 / 20 / 30 within
+// noise on K3': 9.63 / 9.60 / 9.61 ms, profiles/r04/ab/cbm_cost_ab.txt)
+constexpr double CBM_COST = 20.0;
 // IAS_SYM_CBM=0: the partitioned rows take the hash partitions (A/B)
 static bool cbm_enabled() {
     static const bool on = [] {
