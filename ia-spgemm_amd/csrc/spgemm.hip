@@ -2988,63 +2988,90 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     const bool bitmap_sort = nwide > 0 && !force_global && plan->n_cols > 0 && plan->n_cols <= SORTBM_COLS;
     if (bitmap_sort && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * slots + 16ull * nwide + 256));
     if (nwide > 0 && !radix && !bitmap_sort) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
-    int c;
     // one wave per row up to 512 entries (4 rows per workgroup, wave
-    // barriers only), then teams sized so a row fills ~half their slots
-    if ((c = hc.count[1]) > 0)
-        k_sort_bucket<64, 1, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(1), c, ptr, len, stride, col, val);
-    if ((c = hc.count[2]) > 0)
-        k_sort_bucket<64, 4, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(2), c, ptr, len, stride, col, val);
-    if ((c = hc.count[3]) > 0)
-        k_sort_bucket<64, 8, 4><<<grid_for(c, 4), 256, 0, s>>>(lst(3), c, ptr, len, stride, col, val);
-    if ((c = hc.count[4]) > 0)
-        k_sort_bucket<128, 8, 1><<<c, 128, 0, s>>>(lst(4), c, ptr, len, stride, col, val);
-    if ((c = hc.count[5]) > 0)
-        k_sort_bucket<256, 8, 1><<<c, 256, 0, s>>>(lst(5), c, ptr, len, stride, col, val);
-    if ((c = hc.count[6]) > 0)
-        k_sort_bucket<512, 8, 1><<<c, 512, 0, s>>>(lst(6), c, ptr, len, stride, col, val);
-    if ((c = hc.count[7]) > 0)
-        k_sort_bucket<1024, 8, 1><<<c, 1024, 0, s>>>(lst(7), c, ptr, len, stride, col, val);
-    if ((c = hc.count[8]) > 0) {
-        const size_t lds = sortb2_lds((int32_t)plan->n_cols);
-        static bool b2_done = false;
-        allow_lds(k_sort_bitmap16, b2_done, lds);
-        const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap16, SORTBM_T, lds));
-        k_sort_bitmap16<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, s>>>(lst(8), c, ptr, len, stride, col,
-                                                                                     val, (int32_t)plan->n_cols);
+    // barriers only), then teams sized so a row fills ~half their slots.
+    // The bins run on the forked side streams, largest estimated work (rows x
+    // mean entries) first onto the least-loaded stream, as the symbolic bins:
+    // serially they summed to the whole sort pass (K3' 9.9 ms), the
+    // column-bitmap kernels holding one workgroup per CU.
+    auto launch = [&](int b, hipStream_t t) {
+        int c;
+        switch (b) {
+        case 1: c = hc.count[1];
+            k_sort_bucket<64, 1, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(1), c, ptr, len, stride, col, val); break;
+        case 2: c = hc.count[2];
+            k_sort_bucket<64, 4, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(2), c, ptr, len, stride, col, val); break;
+        case 3: c = hc.count[3];
+            k_sort_bucket<64, 8, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(3), c, ptr, len, stride, col, val); break;
+        case 4: c = hc.count[4];
+            k_sort_bucket<128, 8, 1><<<c, 128, 0, t>>>(lst(4), c, ptr, len, stride, col, val); break;
+        case 5: c = hc.count[5];
+            k_sort_bucket<256, 8, 1><<<c, 256, 0, t>>>(lst(5), c, ptr, len, stride, col, val); break;
+        case 6: c = hc.count[6];
+            k_sort_bucket<512, 8, 1><<<c, 512, 0, t>>>(lst(6), c, ptr, len, stride, col, val); break;
+        case 7: c = hc.count[7];
+            k_sort_bucket<1024, 8, 1><<<c, 1024, 0, t>>>(lst(7), c, ptr, len, stride, col, val); break;
+        case 8: {
+            c = hc.count[8];
+            const size_t lds = sortb2_lds((int32_t)plan->n_cols);
+            static bool b2_done = false;
+            allow_lds(k_sort_bitmap16, b2_done, lds);
+            const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap16, SORTBM_T, lds));
+            k_sort_bitmap16<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, t>>>(
+                lst(8), c, ptr, len, stride, col, val, (int32_t)plan->n_cols);
+            break;
+        }
+        default: {   // the wide rows
+            c = nwide;
+            if (bitmap_sort) {
+                char *bp = (char *)plan->bufs[ias_plan::B_TMP4].p;
+                double *wv = (double *)bp;
+                int32_t *wc = (int32_t *)(wv + slots);
+                const size_t lds = sortbm_lds((int32_t)plan->n_cols);
+                static bool sb_done = false;
+                allow_lds(k_sort_bitmap, sb_done, lds);
+                const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap, SORTBM_T, lds));
+                k_sort_bitmap<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, t>>>(
+                    lst(wide), c, coff, ptr, len, stride, col, val, (int32_t)plan->n_cols, wc, wv);
+            } else if (radix) {
+                char *bp = (char *)plan->bufs[ias_plan::B_TMP4].p;
+                double *vin = (double *)bp;
+                double *vout = vin + slots;
+                int64_t *beg = (int64_t *)(vout + slots);
+                int64_t *end = beg + c;
+                int32_t *kin = (int32_t *)(end + c);
+                int32_t *kout = kin + slots;
+                void *tmp = (void *)(((uintptr_t)(kout + slots) + 255) & ~(uintptr_t)255);
+                const dim3 g(c, 16);
+                k_wide_gather<<<g, 256, 0, t>>>(lst(wide), c, coff, ptr, len, stride, col, val, kin, vin, beg,
+                                                end, false);
+                (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, rtmp, (const int32_t *)kin, kout,
+                                                                  (const double *)vin, vout, (int)slots, c,
+                                                                  (const int64_t *)beg, (const int64_t *)end,
+                                                                  0, 31, t);
+                k_wide_gather<<<g, 256, 0, t>>>(lst(wide), c, coff, ptr, len, stride, col, val, kout, vout,
+                                                beg, end, true);
+            } else {
+                k_sort_global<<<c, 1024, 0, t>>>(lst(wide), c, offs, ptr, len, stride, col, val,
+                                                 (char *)plan->bufs[ias_plan::B_TMP4].p);
+            }
+        }
+        }
+    };
+    std::vector<std::pair<double, int>> jobs;
+    for (int b = 1; b <= 8; ++b)
+        if (hc.count[b] > 0) jobs.push_back({(double)hc.count[b] * 0.5 * (double)(u[b - 1] + u[b]), b});
+    if (nwide > 0) jobs.push_back({slots > 0 ? (double)slots : (double)nwide * 16384.0, wide});
+    std::stable_sort(jobs.begin(), jobs.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
+    IAS_TRY(plan->fork());
+    double load[ias_plan::NSIDE] = {};
+    for (const auto &j : jobs) {
+        const int i = (int)(std::min_element(load, load + ias_plan::NSIDE) - load);
+        load[i] += j.first;
+        launch(j.second, (hipStream_t)plan->side_stream(i));
     }
-    if ((c = nwide) > 0 && bitmap_sort) {
-        char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
-        double *wv = (double *)b;
-        int32_t *wc = (int32_t *)(wv + slots);
-        const size_t lds = sortbm_lds((int32_t)plan->n_cols);
-        static bool sb_done = false;
-        allow_lds(k_sort_bitmap, sb_done, lds);
-        const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap, SORTBM_T, lds));
-        k_sort_bitmap<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, s>>>(
-            lst(wide), c, coff, ptr, len, stride, col, val, (int32_t)plan->n_cols, wc, wv);
-    } else if ((c = nwide) > 0 && radix) {
-        char *b = (char *)plan->bufs[ias_plan::B_TMP4].p;
-        double *vin = (double *)b;
-        double *vout = vin + slots;
-        int64_t *beg = (int64_t *)(vout + slots);
-        int64_t *end = beg + c;
-        int32_t *kin = (int32_t *)(end + c);
-        int32_t *kout = kin + slots;
-        void *tmp = (void *)(((uintptr_t)(kout + slots) + 255) & ~(uintptr_t)255);
-        const dim3 g(c, 16);
-        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, coff, ptr, len, stride, col, val, kin, vin, beg,
-                                        end, false);
-        HIPC(hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, rtmp, (const int32_t *)kin, kout,
-                                                         (const double *)vin, vout, (int)slots, c,
-                                                         (const int64_t *)beg, (const int64_t *)end,
-                                                         0, 31, s));
-        k_wide_gather<<<g, 256, 0, s>>>(lst(wide), c, coff, ptr, len, stride, col, val, kout, vout,
-                                        beg, end, true);
-    } else if (c > 0) {
-        k_sort_global<<<c, 1024, 0, s>>>(lst(wide), c, offs, ptr, len, stride, col, val,
-                                         (char *)plan->bufs[ias_plan::B_TMP4].p);
-    }
+    HIPC(hipGetLastError());
+    IAS_TRY(plan->join());
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
 }
