@@ -875,6 +875,9 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         // (two instantiations: a pointer that may be either compiles to flat
         // instructions, which wait on both the LDS and the memory counters)
         const bool own_l = M <= a.own_cap;
+#if IAS_TIMING
+        if (!own_l) tmr.acc[7] += 100;   // phase 7 reads as the share of rows with the global minima table
+#endif
         auto multi = [&](int32_t c) -> bool { return (cbm[c >> 5] >> (c & 31)) & 1u; };
         // rank of a multi column from its superblock's 8 words and prefix
         auto rank_of = [&](int32_t c, const uint4 &x, const uint4 &y, uint32_t sp) -> uint32_t {
