@@ -1902,6 +1902,13 @@ constexpr int32_t WIDE_MIN = (1 << 19) - 1;
 // noise on K3': 9.63 / 9.60 / 9.61 ms, profiles/r04/ab/cbm_cost_ab.txt)
 constexpr double CBM_COST = 20.0;
 // IAS_SYM_CBM=0: the partitioned rows take the hash partitions (A/B)
+static bool sym_feedback() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_SYM_FEEDBACK");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 static bool cbm_enabled() {
     static const bool on = [] {
         const char *e = getenv("IAS_SYM_CBM");
@@ -2356,6 +2363,8 @@ ias_plan::~ias_plan() {
         if (e) hipEventDestroy(e);
     for (auto &e : n2_ev)
         if (e) hipEventDestroy(e);
+    for (auto &e : bin_ev)
+        if (e) hipEventDestroy(e);
     if (host_counters) hipHostFree(host_counters);
     if (own_stream && stream) hipStreamDestroy((hipStream_t)stream);
 }
@@ -2541,16 +2550,29 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // kernel's serial ns per product on K3' (short 5, sym3 3.5, sym4 4.2,
     // sym5 7, bucketed partitions 40: their whole-CU workgroups wait beside
     // the other bins).
+    // From the second call of a plan on, each bin's weight is its measured
+    // duration beside the others per estimated product (the serial weights
+    // left the two queues 0.55 ms apart on K3'); IAS_SYM_FEEDBACK=0: serial
+    // weights only.
     int sym_lane[MAX_BINS] = {};
+    double sym_est[MAX_BINS] = {};
+    const bool fb = !serial && !small && sym_feedback();
+    if (fb && !bin_ev[0])
+        for (auto &e : bin_ev) HIPC(hipEventCreate(&e));
     {
         double load[NSIDE] = {};
         std::vector<std::pair<double, int>> jobs;
-        if (c1.count[sym_part] > 0) jobs.push_back({(cbm ? CBM_COST : 40.0) * (double)c1.part_prod, sym_part});
+        auto weight = [&](int b, double serial_w) { return fb && sym_w[b] > 0.0 ? sym_w[b] : serial_w; };
+        if (c1.count[sym_part] > 0) {
+            sym_est[sym_part] = (double)c1.part_prod;
+            jobs.push_back({weight(sym_part, cbm ? CBM_COST : 40.0) * sym_est[sym_part], sym_part});
+        }
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
                 const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
                 const double w = u <= SHORT_MAX ? 5.0 : u <= SYM3_MAX ? 3.5 : u <= SYM4_MAX ? 4.2 : 7.0;
-                jobs.push_back({w * c1.count[b] * 0.5 * (double)(l + u), b});
+                sym_est[b] = c1.count[b] * 0.5 * (double)(l + u);
+                jobs.push_back({weight(b, w) * sym_est[b], b});
             }
         std::stable_sort(jobs.begin(), jobs.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
         for (const auto &j : jobs) {
@@ -2559,8 +2581,14 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             sym_lane[j.second] = i;
         }
     }
+    auto bin_mark = [&](int b, hipStream_t t, int end) {
+        if (!fb) return;
+        (void)hipEventRecord(bin_ev[2 * b + end], t);
+        bin_rec[b] = true;
+    };
     if ((c = c1.count[sym_part]) > 0) {
         hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
+        bin_mark(sym_part, t, 0);
         if (cbm) {
             static bool cbm_done = false;
             // the minima table takes the LDS left beyond the bitmap (3,968 entries at 2^20 columns)
@@ -2587,47 +2615,54 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                                           sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
             CHECK_LAUNCH("k_symbolic_part", t);
         }
+        bin_mark(sym_part, t, 1);
     }
+    auto launch_sym = [&](int b, int c, hipStream_t t) -> ias_status {
+        const int32_t u = SYM2_BINS[b - 1].upper;
+        if (u <= SHORT_MAX) {
+            const ShortArgs sh{A, ax, B.col, B.val, SL + st[b], c, nnz, sa.dupn};
+            short_sym_launch(u, sh, t);
+            CHECK_LAUNCH("k_short_sym", t);
+            return IAS_SUCCESS;
+        }
+        Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
+                    sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
+        if (!c1.wide_b && u > SYM4_MAX && u <= SYM5_MAX) {
+            const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                              sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                              &dc->s3_retry[b & 15]};
+            sym5_bin(u, a5, a2, t);
+            CHECK_LAUNCH("k_sym5", t);
+            return IAS_SUCCESS;
+        }
+        if (!c1.wide_b && u > SYM3_MAX && u <= SYM4_MAX) {
+            const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                              sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                              &dc->s3_retry[b & 15]};
+            sym4_bin(a4, a2, t);
+            CHECK_LAUNCH("k_sym4", t);
+            return IAS_SUCCESS;
+        }
+        if (!c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
+            const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                              sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                              &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
+            Sym2Args r2 = a2;
+            r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
+            sym3_bin(u, a3, r2, t);
+            CHECK_LAUNCH("k_sym3", t);
+            return IAS_SUCCESS;
+        }
+        sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
+        CHECK_LAUNCH("k_sym2", t);
+        return IAS_SUCCESS;
+    };
     for (int b = ss.nval; b >= 1; --b)
         if ((c = c1.count[b]) > 0) {
             hipStream_t t = (hipStream_t)side_stream(sym_lane[b]);
-            const int32_t u = SYM2_BINS[b - 1].upper;
-            if (u <= SHORT_MAX) {
-                const ShortArgs sh{A, ax, B.col, B.val, SL + st[b], c, nnz, sa.dupn};
-                short_sym_launch(u, sh, t);
-                CHECK_LAUNCH("k_short_sym", t);
-                continue;
-            }
-            Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
-                        sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
-            if (!c1.wide_b && u > SYM4_MAX && u <= SYM5_MAX) {
-                const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
-                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
-                                  &dc->s3_retry[b & 15]};
-                sym5_bin(u, a5, a2, t);
-                CHECK_LAUNCH("k_sym5", t);
-                continue;
-            }
-            if (!c1.wide_b && u > SYM3_MAX && u <= SYM4_MAX) {
-                const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
-                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
-                                  &dc->s3_retry[b & 15]};
-                sym4_bin(a4, a2, t);
-                CHECK_LAUNCH("k_sym4", t);
-                continue;
-            }
-            if (!c1.wide_b && u >= SYM3_MIN && u <= SYM3_MAX) {
-                const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
-                                  sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
-                                  &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
-                Sym2Args r2 = a2;
-                r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
-                sym3_bin(u, a3, r2, t);
-                CHECK_LAUNCH("k_sym3", t);
-                continue;
-            }
-            sym2_bin(SYM2_BINS[b - 1].cfg, a2, t);
-            CHECK_LAUNCH("k_sym2", t);
+            bin_mark(b, t, 0);
+            IAS_TRY(launch_sym(b, c, t));
+            bin_mark(b, t, 1);
         }
     HIPC(hipGetLastError());
     IAS_TRY(join());
@@ -2677,6 +2712,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     HIPC(hipEventRecord(ev[2], s));
     HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + nnz(C), unit counts
     HIPC((hipError_t)host_wait(s));
+    // the symbolic bins are done: their durations for the next call's balance
+    for (int b = 0; b < MAX_BINS; ++b)
+        if (bin_rec[b]) {
+            bin_rec[b] = false;
+            float ms = 0.f;
+            if (sym_est[b] > 0.0 && hipEventElapsedTime(&ms, bin_ev[2 * b], bin_ev[2 * b + 1]) == hipSuccess && ms > 0.f)
+                sym_w[b] = 1e6 * (double)ms / sym_est[b];
+            (void)hipGetLastError();
+        }
     const Counters c2 = hc[1];
     nnz_total = rows > 0 ? (int64_t)c2.nnz_total : 0;
     n2_units = (int64_t)c2.n2_units;

@@ -114,6 +114,12 @@ struct ias_plan {
     int64_t n2_dunits = 0;  //   and up to here to rows with duplicates
     hipEvent_t fix_ev[2] = {}; // units of class 0 / class 1 done: their fix-ups may start
     hipEvent_t n2_ev[6] = {};  // around each streaming-pass launch: ms_stream = their sum
+    // symbolic stream balancing fed back from the previous call: each bin's
+    // measured duration beside the others per estimated product (ns; 0: not
+    // measured yet) and the events around its launches
+    double sym_w[ias::MAX_BINS] = {};
+    hipEvent_t bin_ev[2 * ias::MAX_BINS] = {};
+    bool bin_rec[ias::MAX_BINS] = {};
     unsigned long long num_ws = 0;
     // identity of the operands of the last symbolic() (checked by compute)
     const void *last_a = nullptr, *last_b = nullptr;
