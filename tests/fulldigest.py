@@ -38,9 +38,11 @@ def digest_numpy(row_ptr: np.ndarray, col: np.ndarray, val: np.ndarray) -> int:
         return int(x.sum(dtype=np.uint64)) & MASK64
 
 
-def digest_torch(row_ptr, col, val, chunk: int = 1 << 27) -> int:
+def digest_torch(row_ptr, col, val, chunk: int = 1 << 27, row0: int = 0) -> int:
     """The same digest of a device-resident C (torch tensors: int64 row_ptr,
-    int32 col, float64 val), in chunks of entries."""
+    int32 col, float64 val), in chunks of entries.  row0: the global index of
+    C's first row, for a row block of a larger C — the digest is a sum over
+    entries, so the blocks' digests add up (mod 2^64) to the whole C's."""
     import torch
     dev = col.device
     rp = row_ptr.to(torch.int64) - row_ptr[0].to(torch.int64)
@@ -55,7 +57,7 @@ def digest_torch(row_ptr, col, val, chunk: int = 1 << 27) -> int:
         e = torch.arange(e0, e1, dtype=torch.int64, device=dev)
         r = torch.searchsorted(rp, e, right=True) - 1
         pos = e - rp[r]
-        x = vb[e0:e1] ^ (col[e0:e1].to(torch.int64) * c_col) ^ (pos * c_pos) ^ (r * c_row)
+        x = vb[e0:e1] ^ (col[e0:e1].to(torch.int64) * c_col) ^ (pos * c_pos) ^ ((r + row0) * c_row)
         x = x * c_mul
         x = x ^ ((x >> 32) & lo32)
         total += x.sum()

@@ -28,6 +28,9 @@ CASES = {
     "k2_ell1048576_k16_s7": ("ell", (1 << 20, 16, 7, 0)),
     "k3p_rmat20_ef20_s2": ("rmat", (20, 20.0, 0.45, 0.15, 0.15, 2, 0)),
     "k3_rmat20_ef32_s1": ("rmat", (20, 32.0, 0.45, 0.15, 0.15, 1, 0)),
+    # K4: the 8-GPU configuration (R-MAT 2^23, edge factor 24, seed 3); C has
+    # ~1.2e10 entries (~143 GB), so only the streaming digest is recorded
+    "k4_rmat23_ef24_s3": ("rmat", (23, 24.0, 0.45, 0.15, 0.15, 3, 0)),
 }
 
 

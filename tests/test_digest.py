@@ -40,3 +40,24 @@ def test_torch_digest_equals_numpy():
     got = digest_torch(torch.from_numpy(ref.row_ptr), torch.from_numpy(ref.col), torch.from_numpy(ref.val),
                        chunk=100_000)
     assert got == want
+
+
+def test_digest_adds_over_row_blocks():
+    """A row-block split of C (the K4 shards, tests/test_k4.py) digests to the
+    whole C's digest when each block's rows carry their global index (row0)."""
+    torch = pytest.importorskip("torch")
+    A = ias.gen_rmat(12, 16, seed=1)
+    M = ob.Mat.of(A)
+    ref = ob.csr_mul_csr(M, M)
+    want = digest_numpy(ref.row_ptr, ref.col, ref.val)
+    rp = torch.from_numpy(ref.row_ptr)
+    col, val = torch.from_numpy(ref.col), torch.from_numpy(ref.val)
+    bounds = [0, 7, 700, 2048, 4000, A.rows]
+    total = 0
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        s, e = int(rp[r0]), int(rp[r1])
+        total += digest_torch(rp[r0:r1 + 1], col[s:e], val[s:e], chunk=50_000, row0=r0)
+    assert total % (1 << 64) == want
+    # without the global row index the blocks do not add up
+    s, e = int(rp[700]), int(rp[A.rows])
+    assert digest_torch(rp[:701], col[:s], val[:s]) + digest_torch(rp[700:], col[s:e], val[s:e]) != want

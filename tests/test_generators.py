@@ -20,7 +20,7 @@ def stats(golden_dir):
         return json.load(f)
 
 
-@pytest.mark.parametrize("name", [k for k in mg.CASES if not k.startswith("k3")])
+@pytest.mark.parametrize("name", [k for k in mg.CASES if not k.startswith(("k3", "k4"))])
 def test_small_generators(stats, name):
     kind, args = mg.CASES[name]
     A = mg.make(kind, args)
@@ -29,10 +29,11 @@ def test_small_generators(stats, name):
     assert mg.digest(A) == rec["sha256"]
 
 
-@pytest.mark.parametrize("name", ["k3p_rmat20_ef20_s2", "k3_rmat20_ef32_s1"])
+@pytest.mark.parametrize("name", ["k3p_rmat20_ef20_s2", "k3_rmat20_ef32_s1", "k4_rmat23_ef24_s3"])
 def test_headline_matrix(stats, name):
-    """K3' (north-star headline, 2^20 rows, ~20 nnz/row) and K3 (avg 32/row,
-    nnz(C) > 2^31): same bytes every run."""
+    """K3' (north-star headline, 2^20 rows, ~20 nnz/row), K3 (avg 32/row,
+    nnz(C) > 2^31) and K4 (2^23 rows, avg 24/row, the 8-GPU configuration):
+    same bytes every run."""
     kind, args = mg.CASES[name]
     A = mg.make(kind, args)
     rec = stats[name]
