@@ -616,11 +616,37 @@ extern "C" ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_di
     return dia_mul(A, B, C, opts, rep, false);
 }
 
+// [p, p + a) and [q, q + b) share a byte
+static bool overlaps(const void *p, size_t a, const void *q, size_t b) {
+    if (!p || !q || a == 0 || b == 0) return false;
+    const uintptr_t x = (uintptr_t)p, y = (uintptr_t)q;
+    return x < y + b && y < x + a;
+}
+
 extern "C" ias_status ias_dia_mul_dia_into(const ias_dia *A, const ias_dia *B, ias_dia *C,
                                            const ias_opts *opts, ias_report *rep) {
-    if (!C || C->memory != IAS_MEMORY_DEVICE || C->num_diagonals < 0 || !C->diagonal_ind ||
-        (C->num_diagonals > 0 && (!C->diagonal_offsets || !C->val)))
+    if (!A || !B || !C || C->memory != IAS_MEMORY_DEVICE || C->num_diagonals < 0 || !C->diagonal_ind ||
+        (C->num_diagonals > 0 && (!C->diagonal_offsets || !C->val)) || A->num_diagonals < 0 ||
+        B->num_diagonals < 0 || A->rows < 0 || A->cols < 0 || B->cols < 0)
         return IAS_ERROR_INVALID_ARGUMENT;
+    // C is written in place while A and B are read: no array of C may share
+    // memory with one of theirs (C = A would race the kernel's reads)
+    const size_t cr = (size_t)A->rows, ccols = (size_t)B->cols;
+    const size_t c_bytes[3] = {8 * cr * (size_t)C->num_diagonals, 4 * (size_t)C->num_diagonals,
+                               4 * (cr + ccols > 0 ? cr + ccols - 1 : 0)};
+    const void *c_arr[3] = {C->val, C->diagonal_offsets, C->diagonal_ind};
+    for (const ias_dia *X : {A, B}) {
+        const size_t xr = (size_t)X->rows, xc = (size_t)X->cols;
+        const size_t x_bytes[3] = {8 * xr * (size_t)X->num_diagonals, 4 * (size_t)X->num_diagonals,
+                                   4 * (xr + xc > 0 ? xr + xc - 1 : 0)};
+        const void *x_arr[3] = {X->val, X->diagonal_offsets, X->diagonal_ind};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j)
+                if (overlaps(c_arr[i], c_bytes[i], x_arr[j], x_bytes[j])) {
+                    set_last_error("ias_dia_mul_dia_into: C's arrays overlap an operand's");
+                    return IAS_ERROR_INVALID_ARGUMENT;
+                }
+    }
     ias_opts o;
     ias_opts_default(&o);
     if (opts) o = *opts;
@@ -629,7 +655,10 @@ extern "C" ias_status ias_dia_mul_dia_into(const ias_dia *A, const ias_dia *B, i
 }
 
 extern "C" ias_status ias_dia_mul_dia_ndiag(const ias_dia *A, const ias_dia *B, int32_t *nd_c) {
-    if (!A || !B || !nd_c) return IAS_ERROR_INVALID_ARGUMENT;
+    if (!A || !B || !nd_c || A->num_diagonals < 0 || B->num_diagonals < 0 ||
+        (A->num_diagonals > 0 && !A->diagonal_offsets) || (B->num_diagonals > 0 && !B->diagonal_offsets))
+        return IAS_ERROR_INVALID_ARGUMENT;
+    if (!A->choice || !B->choice) return IAS_ERROR_INFEASIBLE;   // as dia_mul
     if (A->cols != B->rows) return IAS_ERROR_DIMENSION_MISMATCH;
     std::vector<int32_t> offa(A->num_diagonals), offb(B->num_diagonals);
     for (auto xo : {std::make_pair(A, &offa), std::make_pair(B, &offb)}) {

@@ -19,6 +19,8 @@
 namespace ias {
 
 static thread_local char g_last_error[512] = "";
+static thread_local uint32_t g_last_diag = 0u;
+void set_last_diag(uint32_t flags) { g_last_diag = flags; }
 
 void set_last_error(const char *fmt, ...) {
     va_list ap;
@@ -61,18 +63,30 @@ struct BlockCache {
     std::map<void *, size_t> size_of;                           // cached-class blocks in use or free
     // freed blocks whose last users may still run: they join `free` after one
     // device-wide synchronisation, taken when an allocation would reuse them
-    // (one sync per call that allocates, not one per freed array)
-    std::vector<std::pair<void *, size_t>> pending[64];
+    // (one sync per call that allocates, not one per freed array).  Each
+    // pending block is numbered from a per-device counter that only grows;
+    // a sync settles exactly the blocks numbered below the counter's value
+    // read before it (another thread may settle or queue blocks meanwhile, so
+    // positions in the vector mean nothing).
+    struct Pending {
+        void *p;
+        size_t size;
+        uint64_t seq;
+    };
+    std::vector<Pending> pending[64];
+    uint64_t next_seq[64] = {};
     size_t held[64] = {};
-    // pending blocks whose last users were queued before a device sync that
-    // then completed -> free (caller holds the lock; `n` = the size of
-    // pending[device] taken under the lock BEFORE that sync: blocks freed by
-    // another thread after the snapshot may still be in use and stay pending)
-    void settle(int device, size_t n) {
-        auto &p = pending[device];
-        n = std::min(n, p.size());
-        for (size_t i = 0; i < n; ++i) free[{device, p[i].second}].push_back(p[i].first);
-        p.erase(p.begin(), p.begin() + (ptrdiff_t)n);
+    // pending blocks queued before a device sync that then completed -> free
+    // (caller holds the lock; `upto` = next_seq[device] read under the lock
+    // BEFORE that sync)
+    void settle(int device, uint64_t upto) {
+        auto &v = pending[device];
+        size_t k = 0;
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (v[i].seq < upto) free[{device, v[i].size}].push_back(v[i].p);
+            else v[k++] = v[i];
+        }
+        v.resize(k);
     }
     static size_t round(size_t b) {
         size_t r = 256;
@@ -83,10 +97,10 @@ struct BlockCache {
     size_t trim(int device) {
         std::vector<void *> drop;
         size_t bytes = 0;
-        size_t snap;
+        uint64_t snap;
         {
             std::lock_guard<std::mutex> g(mu);
-            snap = pending[device].size();
+            snap = next_seq[device];
         }
         (void)hipDeviceSynchronize();
         {
@@ -129,7 +143,7 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
     const size_t want = cached ? BlockCache::round(bytes) : bytes;
     if (cached) {
         bool sync = false;
-        size_t snap = 0;
+        uint64_t snap = 0;
         {
             std::lock_guard<std::mutex> g(c.mu);
             auto it = c.free.find({device, want});
@@ -139,8 +153,8 @@ ias_status dev_alloc(void **p, size_t bytes, int device) {
                 c.held[device] -= want;
                 return IAS_SUCCESS;
             }
-            for (auto &b : c.pending[device]) sync = sync || b.second == want;
-            snap = c.pending[device].size();
+            for (auto &b : c.pending[device]) sync = sync || b.size == want;
+            snap = c.next_seq[device];
         }
         if (sync) {
             // a freed block of this size exists: wait for its last users (only
@@ -189,7 +203,7 @@ ias_status dev_free(void *p, int device) {
         // allocation synchronises the device (dev_alloc)
         std::lock_guard<std::mutex> g(c.mu);
         const size_t r = c.size_of[p];
-        c.pending[device].push_back({p, r});
+        c.pending[device].push_back({p, r, c.next_seq[device]++});
         c.held[device] += r;
         return IAS_SUCCESS;
     }
@@ -279,6 +293,7 @@ extern "C" const char *ias_status_string(ias_status s) {
 }
 
 extern "C" const char *ias_last_error(void) { return g_last_error; }
+extern "C" uint32_t ias_last_diag(void) { return g_last_diag; }
 
 extern "C" ias_status ias_device_count(int32_t *count) {
     if (!count) return IAS_ERROR_INVALID_ARGUMENT;

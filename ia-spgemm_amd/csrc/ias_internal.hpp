@@ -34,6 +34,7 @@ int host_wait(void *stream);
 
 // Record the last HIP/internal error message for ias_status_string's detail.
 void set_last_error(const char *fmt, ...);
+void set_last_diag(uint32_t flags);   // ias_last_diag() of the calling thread
 
 inline bool is_device(int32_t memory) { return memory == IAS_MEMORY_DEVICE; }
 

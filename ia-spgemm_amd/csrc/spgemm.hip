@@ -724,7 +724,20 @@ struct CbmArgs {
     int32_t *dupn, *gdupt;
     int32_t div, dmax;
     int32_t own_cap;   // LDS words beyond the bitmap + prefixes (the minima table when it fits)
+    int32_t force;     // test knob (IAS_CBM_FORCE): CBM_NO_LIST / CBM_NO_LWORDS force those branches
+    uint32_t *hits;    // test knob: the branches the rows took (CBM_HIT_*, OR-ed), or nullptr
 };
+// IAS_CBM_FORCE bits (own_cap = 0 forces the global minima table) and the
+// branch flags k_sym_cbm ORs into CbmArgs::hits
+constexpr int32_t CBM_GLOBAL_OWN = 1, CBM_NO_LIST = 2, CBM_NO_LWORDS = 4;
+constexpr uint32_t CBM_HIT_GLOBAL_OWN = 1, CBM_HIT_UNLISTED_KEEP = 2, CBM_HIT_UNLISTED_DROP = 4,
+                   CBM_HIT_GLOBAL_WORDS = 8, CBM_HIT_LISTED_KEEP = 16, CBM_HIT_LISTED_DROP = 32,
+                   CBM_HIT_LDS_OWN = 64;
+static_assert(CBM_HIT_GLOBAL_OWN == IAS_DIAG_CBM_GLOBAL_OWN && CBM_HIT_UNLISTED_KEEP == IAS_DIAG_CBM_UNLISTED_KEEP &&
+                  CBM_HIT_UNLISTED_DROP == IAS_DIAG_CBM_UNLISTED_DROP &&
+                  CBM_HIT_GLOBAL_WORDS == IAS_DIAG_CBM_GLOBAL_WORDS && CBM_HIT_LISTED_KEEP == IAS_DIAG_CBM_LISTED_KEEP &&
+                  CBM_HIT_LISTED_DROP == IAS_DIAG_CBM_LISTED_DROP && CBM_HIT_LDS_OWN == IAS_DIAG_CBM_LDS_OWN,
+              "ias_last_diag flags");
 
 // Workgroup-only sharing in k_sym_cbm: plain stores and loads meet in the
 // CU's L1 after a barrier; values changed by global atomics (performed in
@@ -836,6 +849,7 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     int M = 0;   // columns of more than one product
     uint2 *pairs = nullptr;   // the duplicates (product, first touch) when kept
     bool lwords = false;      // first-touch words in LDS (over the dead column bitmap)
+    uint32_t hit = 0u;        // branches taken (test knob)
     auto full_word = [&](int32_t i) -> uint32_t {
         return (i < W - 1 || (P & 31) == 0) ? ~0u : ((1u << (P & 31)) - 1u);
     };
@@ -946,9 +960,12 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         tmr.mark(3);
         // ---- 4. duplicates: clear their first-touch bits, list (product, first touch)
         const int32_t nml = ncnt[2];
-        const bool listed = nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
+        const bool listed = !(a.force & CBM_NO_LIST) && nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
         pairs = (uint2 *)(wk + (listed ? m0 + 2 * nml : m0));
-        lwords = listed && W <= NCW;
+        lwords = listed && W <= NCW && !(a.force & CBM_NO_LWORDS);
+        hit = (OL ? CBM_HIT_LDS_OWN : CBM_HIT_GLOBAL_OWN) | (lwords ? 0u : CBM_HIT_GLOBAL_WORDS) |
+              (listed ? (keep ? CBM_HIT_LISTED_KEEP : CBM_HIT_LISTED_DROP)
+                      : (keep ? CBM_HIT_UNLISTED_KEEP : CBM_HIT_UNLISTED_DROP));
         if (lwords) {
             for (int32_t i = tid; i < W; i += CBM_BLOCK) cbm[i] = full_word(i);
             __syncthreads();
@@ -1053,6 +1070,7 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     if (tid == 0) {
         a.nnz_row[row] = nnz;
         a.dupn[row] = keep ? nd : -1;
+        if (a.hits && hit) atomicOr(a.hits, hit);
     }
     tmr.mark(6);
     tmr.flush(28, tid == 0);   // slot 28: column-bitmap symbolic
@@ -1413,6 +1431,30 @@ __device__ __forceinline__ void bitonic(int32_t *sk, double *sv, uint32_t cap) {
     }
 }
 
+// keys only (distinct int32), ascending
+template <int TEAM>
+__device__ __forceinline__ void bitonic_keys(int32_t *sk, uint32_t cap) {
+    const int lane = Team<TEAM>::lane();
+    for (uint32_t k = 2; k <= cap; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < cap; i += TEAM) {
+                const uint32_t ixj = i ^ j;
+                if (ixj > i) {
+                    const bool up = (i & k) == 0;
+                    const int32_t a = sk[i], b = sk[ixj];
+                    if ((a > b) == up) {
+                        sk[i] = b;
+                        sk[ixj] = a;
+                    }
+                }
+            }
+            Team<TEAM>::sync();
+        }
+    }
+}
+// a bucket of more keys than this sends the row to bitonic_keys (8x the mean of 4)
+constexpr uint32_t SORTB_HEAVY = 32;
+
 __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t *len, int64_t stride,
                                               int64_t row, int64_t &o, int32_t &n) {
     if (ptr) {
@@ -1510,17 +1552,24 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
         if (e < n) pib[k] = atomicAdd(&hist[team][b[k]], 1u);
     }
     TM::sync();
-    // bucket starts: exclusive scan of the counts (NBT per thread, in order)
+    // bucket starts: exclusive scan of the counts (NBT per thread, in order);
+    // bits 16+ of the scanned value count the lanes holding a bucket of more
+    // than SORTB_HEAVY keys (clustered columns with a far outlier put most of
+    // the row into a few buckets, and the in-bucket rank loop is quadratic)
+    bool heavy;
     {
         uint32_t cnt[NBT], sum = 0;
+        bool big = false;
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
             cnt[j] = i < nb ? hist[team][i] : 0u;
             sum += cnt[j];
+            big = big || cnt[j] > SORTB_HEAVY;
         }
         int tot;
-        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, scratch[team]);
+        uint32_t run = (uint32_t)TM::excl_sum((int)(sum | (big ? 1u << 16 : 0u)), tot, scratch[team]) & 0xffffu;
+        heavy = (tot >> 16) != 0;
         TM::sync();   // every count read before the starts overwrite them
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
@@ -1531,19 +1580,46 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
         if (lane == 0) hist[team][nb] = (uint32_t)n;
     }
     TM::sync();
-#pragma unroll
-    for (int k = 0; k < E; ++k)
-        if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
-    TM::sync();
     uint32_t r[E];
+    if (!heavy) {
 #pragma unroll
-    for (int k = 0; k < E; ++k) {
-        r[k] = 0u;
-        if (k * TEAM + lane >= n) continue;
-        const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
-        uint32_t x = s0;
-        for (uint32_t j = s0; j < s1; ++j) x += sk[team][j] < c[k] ? 1u : 0u;
-        r[k] = x;
+        for (int k = 0; k < E; ++k)
+            if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
+        TM::sync();
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            r[k] = 0u;
+            if (k * TEAM + lane >= n) continue;
+            const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
+            uint32_t x = s0;
+            for (uint32_t j = s0; j < s1; ++j) x += sk[team][j] < c[k] ? 1u : 0u;
+            r[k] = x;
+        }
+    } else {
+        // skewed buckets: the keys alone sorted in LDS (bitonic, padded to a
+        // power of two), each entry's rank by a binary search of its key —
+        // the keys are distinct, so the rank is exact
+        uint32_t cap = 1;
+        while (cap < (uint32_t)n) cap <<= 1;
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            const int e = k * TEAM + lane;
+            if ((uint32_t)e < cap) sk[team][e] = e < n ? c[k] : INT32_MAX;
+        }
+        TM::sync();
+        bitonic_keys<TEAM>(sk[team], cap);
+#pragma unroll
+        for (int k = 0; k < E; ++k) {
+            r[k] = 0u;
+            if (k * TEAM + lane >= n) continue;
+            uint32_t lo2 = 0, hi2 = (uint32_t)n;   // first key >= c[k]
+            while (lo2 < hi2) {
+                const uint32_t mid = (lo2 + hi2) >> 1;
+                if (sk[team][mid] < c[k]) lo2 = mid + 1;
+                else hi2 = mid;
+            }
+            r[k] = lo2;
+        }
     }
     if constexpr (!STAGE) {
 #pragma unroll
@@ -2591,14 +2667,21 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         bin_mark(sym_part, t, 0);
         if (cbm) {
             static bool cbm_done = false;
-            // the minima table takes the LDS left beyond the bitmap (3,968 entries at 2^20 columns)
-            const int32_t own_cap = (int32_t)std::max<int64_t>(0, ((int64_t)160 * 1024 - 512 - (int64_t)cbm_lds_bytes(ncw)) / 4);
-            const size_t lds = cbm_lds_bytes(ncw) + 4ull * own_cap;
+            // the minima table takes the LDS left beyond the bitmap (3,968
+            // entries at 2^20 columns); IAS_CBM_FORCE (test knob, read per
+            // call): forced branches (CBM_GLOBAL_OWN: no LDS table) and the
+            // branch flags collected for ias_last_diag()
+            const char *fe = getenv("IAS_CBM_FORCE");
+            const int32_t force = fe && *fe ? (int32_t)atoi(fe) : 0;
+            const int32_t own_lds = (int32_t)std::max<int64_t>(0, ((int64_t)160 * 1024 - 512 - (int64_t)cbm_lds_bytes(ncw)) / 4);
+            const int32_t own_cap = (force & CBM_GLOBAL_OWN) ? 0 : own_lds;
+            const size_t lds = cbm_lds_bytes(ncw) + 4ull * own_lds;
             allow_lds(k_sym_cbm, cbm_done, lds);
             k_expand_flat<<<dim3((unsigned)c, 4), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                as<int32_t>(bufs[B_TCOL]));
             const CbmArgs ca{tcol, SL + st[sym_part], ncw, as<uint2>(bufs[B_PBKT]), bm, nnz,
-                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, own_cap};
+                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, own_cap, force,
+                             fe && *fe ? (uint32_t *)&dc2->cbm_hits : nullptr};
             k_sym_cbm<<<c, CBM_BLOCK, lds, t>>>(ca);
             CHECK_LAUNCH("k_sym_cbm", t);
         } else {
@@ -2736,6 +2819,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     st_prod = (int64_t)c2.st_prod;
     st_nnz = (int64_t)c2.st_nnz;
     max_nnz = c2.max_nnz;
+    set_last_diag((uint32_t)c2.cbm_hits);
     if (rep) {
         float a = 0, b = 0;
         hipEventElapsedTime(&a, ev[0], ev[1]);
@@ -3041,7 +3125,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     // mean entries) first onto the least-loaded stream, as the symbolic bins:
     // serially they summed to the whole sort pass (K3' 9.9 ms), the
     // column-bitmap kernels holding one workgroup per CU.
-    auto launch = [&](int b, hipStream_t t) {
+    auto launch = [&](int b, hipStream_t t) -> hipError_t {
         int c;
         switch (b) {
         case 1: c = hc.count[1];
@@ -3092,10 +3176,10 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
                 const dim3 g(c, 16);
                 k_wide_gather<<<g, 256, 0, t>>>(lst(wide), c, coff, ptr, len, stride, col, val, kin, vin, beg,
                                                 end, false);
-                (void)hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, rtmp, (const int32_t *)kin, kout,
-                                                                  (const double *)vin, vout, (int)slots, c,
-                                                                  (const int64_t *)beg, (const int64_t *)end,
-                                                                  0, 31, t);
+                const hipError_t e = hipcub::DeviceSegmentedRadixSort::SortPairs(
+                    tmp, rtmp, (const int32_t *)kin, kout, (const double *)vin, vout, (int)slots, c,
+                    (const int64_t *)beg, (const int64_t *)end, 0, 31, t);
+                if (e != hipSuccess) return e;
                 k_wide_gather<<<g, 256, 0, t>>>(lst(wide), c, coff, ptr, len, stride, col, val, kout, vout,
                                                 beg, end, true);
             } else {
@@ -3104,6 +3188,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
             }
         }
         }
+        return hipGetLastError();
     };
     std::vector<std::pair<double, int>> jobs;
     for (int b = 1; b <= 8; ++b)
@@ -3112,13 +3197,17 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     std::stable_sort(jobs.begin(), jobs.end(), [](const auto &x, const auto &y) { return x.first > y.first; });
     IAS_TRY(plan->fork());
     double load[ias_plan::NSIDE] = {};
+    hipError_t le = hipSuccess;
     for (const auto &j : jobs) {
         const int i = (int)(std::min_element(load, load + ias_plan::NSIDE) - load);
         load[i] += j.first;
-        launch(j.second, (hipStream_t)plan->side_stream(i));
+        if (le == hipSuccess) le = launch(j.second, (hipStream_t)plan->side_stream(i));
     }
-    HIPC(hipGetLastError());
-    IAS_TRY(plan->join());
+    IAS_TRY(plan->join());   // the side streams join the plan stream even after a failed launch
+    if (le != hipSuccess) {
+        set_last_error("row sort launch failed: %s", hipGetErrorString(le));
+        return le == hipErrorOutOfMemory ? IAS_ERROR_OUT_OF_MEMORY : IAS_ERROR_DEVICE;
+    }
     HIPC(hipGetLastError());
     return IAS_SUCCESS;
 }

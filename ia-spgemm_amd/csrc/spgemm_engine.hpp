@@ -49,7 +49,7 @@ struct Counters {
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
-    int32_t pad;
+    int32_t cbm_hits;             // k_sym_cbm branches taken (IAS_CBM_FORCE set: ias_last_diag)
     int32_t s3_retry[16];         // sym3 / sym4: rows handed to sym2, per bin (bin & 15; retry lists)
     int32_t wide_b;               // a selected B row ends beyond 2^30 entries: no sym3 (32-bit offsets)
     int32_t count[MAX_BINS];      // rows per bin (counting pass)

@@ -93,7 +93,7 @@ class MtxInfo(C.Structure):
 
 # every symbol include/ias.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "ias_abi_version", "ias_status_string", "ias_device_count", "ias_opts_default",
+    "ias_abi_version", "ias_status_string", "ias_last_diag", "ias_device_count", "ias_opts_default",
     "ias_plan_create", "ias_plan_destroy",
     "ias_csr_alloc", "ias_csr_copy", "ias_csr_free", "ias_coo_free", "ias_ell_free", "ias_dia_free",
     "ias_coo_copy", "ias_ell_copy", "ias_dia_copy",
@@ -125,6 +125,7 @@ def _load():
         "ias_abi_version": (C.c_int, []),
         "ias_status_string": (C.c_char_p, [C.c_int]),
         "ias_last_error": (C.c_char_p, []),
+        "ias_last_diag": (C.c_uint32, []),
         "ias_device_count": (C.c_int, [i32p]),
         "ias_opts_default": (None, [P(Opts)]),
         "ias_plan_create": (C.c_int, [P(C.c_void_p), C.c_int32, C.c_void_p]),

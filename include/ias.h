@@ -32,10 +32,11 @@
 extern "C" {
 #endif
 
-#define IAS_ABI_VERSION 5   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
+#define IAS_ABI_VERSION 6   /* 2: ias_report gained ms_stream, stream_products, stream_nnz;
                                3: ias_csr_mul_csr_into (single pass);
                                4: input-aware selector (features, images, MatNet);
-                               5: ias_report.stream_launches */
+                               5: ias_report.stream_launches;
+                               6: ias_last_diag */
 
 typedef enum ias_status {
     IAS_SUCCESS = 0,
@@ -165,6 +166,20 @@ int         ias_abi_version(void);
 const char *ias_status_string(ias_status s);
 /* Detail of the last failure on the calling thread ("" if none). */
 const char *ias_last_error(void);
+/* Diagnostics of the calling thread's last symbolic pass (the nnz phase of a
+ * CSR product): with the environment variable IAS_CBM_FORCE set (a test knob:
+ * bits 1 = the column-bitmap symbolic's minima table in global memory,
+ * 2 = its duplicates found by a sweep instead of the list, 4 = its first-touch
+ * words in global memory; 0 = no forcing), the OR of the IAS_DIAG_CBM_*
+ * branches its rows took; 0 otherwise.  No reference counterpart. */
+uint32_t    ias_last_diag(void);
+#define IAS_DIAG_CBM_GLOBAL_OWN    1u   /* minima table in the row's work space */
+#define IAS_DIAG_CBM_UNLISTED_KEEP 2u   /* duplicate sweep, duplicates kept for the fix-ups */
+#define IAS_DIAG_CBM_UNLISTED_DROP 4u   /* duplicate sweep, row left to the table path */
+#define IAS_DIAG_CBM_GLOBAL_WORDS  8u   /* first-touch words built in global memory */
+#define IAS_DIAG_CBM_LISTED_KEEP  16u   /* duplicate list, duplicates kept */
+#define IAS_DIAG_CBM_LISTED_DROP  32u   /* duplicate list, row left to the table path */
+#define IAS_DIAG_CBM_LDS_OWN      64u   /* minima table in LDS */
 ias_status  ias_device_count(int32_t *count);
 void        ias_opts_default(ias_opts *opts);
 
@@ -260,8 +275,11 @@ ias_status ias_dia_mul_dia(const ias_dia *A, const ias_dia *B, ias_dia *C,
  * diagonal_offsets >= capacity entries, diagonal_ind >= rows + cols - 1, val >=
  * rows x capacity.  On success C->num_diagonals = nd_C and val is rows x nd_C
  * row-major; a capacity below nd_C returns IAS_ERROR_INSUFFICIENT_CAPACITY with
- * C->num_diagonals = nd_C.  ias_dia_mul_dia_ndiag gives nd_C from the offsets
- * alone (dia:107-140's reachability rule). */
+ * C->num_diagonals = nd_C.  C's arrays must not share memory with A's or B's
+ * (C is written while they are read): IAS_ERROR_INVALID_ARGUMENT.
+ * ias_dia_mul_dia_ndiag gives nd_C from the offsets alone (dia:107-140's
+ * reachability rule; IAS_ERROR_INFEASIBLE for an infeasible operand, as the
+ * product itself). */
 ias_status ias_dia_mul_dia_into(const ias_dia *A, const ias_dia *B, ias_dia *C,
                                 const ias_opts *opts, ias_report *report);
 ias_status ias_dia_mul_dia_ndiag(const ias_dia *A, const ias_dia *B, int32_t *nd_c);

@@ -40,7 +40,7 @@ def test_only_c_symbols_exported():
 
 
 def test_version_and_status_strings():
-    assert ias.lib.ias_abi_version() == 5
+    assert ias.lib.ias_abi_version() == 6
     for s in range(12):
         assert ias.lib.ias_status_string(s)
     assert ias.lib.ias_status_string(99) == b"unknown status"

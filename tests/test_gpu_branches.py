@@ -1,0 +1,236 @@
+"""Targeted GPU tests of branches the full-size inputs do not reach (or reach
+without an entry-by-entry check), each bitwise against the oracle's
+CSR_MUL_CSR restatement (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:85-193):
+
+  * the column-bitmap symbolic (k_sym_cbm) of rows beyond 16,384 products:
+    every branch — minima table in LDS or in the row's work space, duplicates
+    found from the list or by a sweep, kept for the fix-ups or left to the
+    table path, first-touch words in LDS or in global memory — natural and
+    forced (IAS_CBM_FORCE), asserted reached through ias_last_diag();
+  * the LDS bucket sort (IAS_ORDER_SORTED) on rows whose columns cluster with
+    far outliers (most keys in a few buckets: the bitonic-keys fallback);
+  * ias_dia_mul_dia_into refusing a C that shares memory with an operand, and
+    ias_dia_mul_dia_ndiag refusing invalid operands;
+  * the block cache of library-allocated device outputs under several host
+    threads allocating and freeing at once.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import ias
+import oracle_bind as ob
+
+pytestmark = pytest.mark.gpu
+
+GLOBAL_OWN, UNLISTED_KEEP, UNLISTED_DROP, GLOBAL_WORDS, LISTED_KEEP, LISTED_DROP, LDS_OWN = 1, 2, 4, 8, 16, 32, 64
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if ias.device_count() < 1:
+        pytest.fail("no HIP device visible: the gpu tests must run on an MI355X box")
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float64).view(np.int64)
+
+
+def assert_csr_identical(got, ref, what=""):
+    assert got.rows == ref.rows and got.cols == ref.cols, what
+    np.testing.assert_array_equal(got.row_ptr, ref.row_ptr, err_msg=f"{what} row_ptr")
+    np.testing.assert_array_equal(got.col, ref.col, err_msg=f"{what} col order")
+    np.testing.assert_array_equal(bits(got.val), bits(ref.val), err_msg=f"{what} values (bitwise)")
+
+
+def _csr(rows, ncol, rng):
+    rp = np.zeros(len(rows) + 1, np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.uniform(-1.0, 1.0, size=col.size)
+    return ias.HostCsr(len(rows), ncol, rp, col, val)
+
+
+def cbm_rows(seed=17):
+    """A*B with B 2^20 columns wide (one LDS column bitmap, 3,968 LDS minima
+    slots beside it) whose first A rows exceed 16,384 products (k_sym_cbm):
+    each takes `prods` products from B rows of 100 columns drawn from a pool
+    of `pool` columns — (P, pool):
+      (60000, 200000) ~7.4k repeated columns > 3,968: global minima, ~8k
+                      duplicates <= P/4: listed, kept;
+      (40000,  40000) global minima, ~15k duplicates > P/4: listed, dropped;
+      (40000,   5000) global minima, 35k duplicates: unlisted, dropped;
+      (30000, 250000) few repeated columns: LDS minima, listed, kept;
+      (20000,   1000) LDS minima, 19k duplicates: unlisted, dropped;
+    then 1,500 ordinary rows."""
+    rng = np.random.default_rng(seed)
+    per = 100
+    brows, arows = [], []
+    for prods, pool in [(60000, 200000), (40000, 40000), (40000, 5000), (30000, 250000), (20000, 1000)]:
+        base = len(brows)
+        for _ in range(prods // per):
+            brows.append(rng.choice(pool, per, replace=False))
+        arows.append(np.arange(base, len(brows)))
+    nb = len(brows)
+    for _ in range(3000):
+        brows.append(rng.choice(1 << 20, 12, replace=False))
+    for _ in range(1500):
+        arows.append(rng.choice(np.arange(nb, len(brows)), 8, replace=False))
+    return _csr(arows, len(brows), rng), _csr(brows, 1 << 20, rng)
+
+
+@pytest.fixture(scope="module")
+def cbm_case():
+    A, B = cbm_rows()
+    return A, B, ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+
+
+# (IAS_CBM_FORCE, branches that must have run)
+FORCED = [
+    (0, GLOBAL_OWN | LDS_OWN | LISTED_KEEP | LISTED_DROP | UNLISTED_DROP),
+    (1, GLOBAL_OWN | LISTED_KEEP | LISTED_DROP | UNLISTED_DROP),          # every row's minima in global memory
+    (2, GLOBAL_OWN | LDS_OWN | UNLISTED_KEEP | UNLISTED_DROP | GLOBAL_WORDS),   # no list: sweeps
+    (4, GLOBAL_WORDS | LISTED_KEEP | LISTED_DROP),                        # listed rows' words in global memory
+    (3, GLOBAL_OWN | UNLISTED_KEEP | UNLISTED_DROP | GLOBAL_WORDS),
+    (5, GLOBAL_OWN | GLOBAL_WORDS | LISTED_KEEP | LISTED_DROP),
+    (7, GLOBAL_OWN | UNLISTED_KEEP | UNLISTED_DROP | GLOBAL_WORDS),
+]
+
+
+@pytest.mark.parametrize("force,want", FORCED, ids=[f"force{f}" for f, _ in FORCED])
+def test_cbm_branches(cbm_case, monkeypatch, force, want):
+    A, B, ref = cbm_case
+    monkeypatch.setenv("IAS_CBM_FORCE", str(force))
+    got, rep = ias.spgemm(A, B)
+    hits = int(ias.lib.ias_last_diag())
+    assert rep.max_row_products == 60000
+    assert_csr_identical(got, ref, f"column-bitmap symbolic, IAS_CBM_FORCE={force}")
+    assert hits & want == want, f"branches reached {hits:#x}, wanted {want:#x}"
+    if force & 1:
+        assert not hits & LDS_OWN
+    if force & 2:
+        assert not hits & (LISTED_KEEP | LISTED_DROP)
+    # and the same product in sorted order (rows of the bitmap path sorted after)
+    if force == 7:
+        got_s, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+        for i in range(5):
+            s, e = ref.row_ptr[i], ref.row_ptr[i + 1]
+            o = np.argsort(ref.col[s:e], kind="stable")
+            np.testing.assert_array_equal(got_s.col[s:e], ref.col[s:e][o])
+            np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))
+
+
+def test_cbm_diag_off_without_knob(cbm_case, monkeypatch):
+    A, B, ref = cbm_case
+    monkeypatch.delenv("IAS_CBM_FORCE", raising=False)
+    got, _ = ias.spgemm(A, B)
+    assert_csr_identical(got, ref, "column-bitmap symbolic")
+    assert ias.lib.ias_last_diag() == 0
+
+
+def skewed_rows(seed=23):
+    """C rows whose columns cluster with far outliers, for every bucket-sort
+    team size (rows of ~100 .. ~8,000 entries): A row i takes m_i B rows whose
+    columns lie in [0, 20000) except one column near 2^20 - 1."""
+    rng = np.random.default_rng(seed)
+    brows = [np.concatenate([rng.choice(20000, 15, replace=False), [(1 << 20) - 1 - i]]) for i in range(3000)]
+    arows = [rng.choice(3000, m, replace=False) for m in (8, 30, 60, 120, 250, 500, 1000, 2000)]
+    arows += [rng.choice(3000, 10, replace=False) for _ in range(200)]
+    return _csr(arows, 3000, rng), _csr(brows, 1 << 20, rng)
+
+
+def test_sort_skewed_buckets():
+    A, B = skewed_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    got, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+    np.testing.assert_array_equal(got.row_ptr, ref.row_ptr)
+    assert int(np.diff(ref.row_ptr).max()) > 4096
+    for i in range(A.rows):
+        s, e = ref.row_ptr[i], ref.row_ptr[i + 1]
+        o = np.argsort(ref.col[s:e], kind="stable")
+        np.testing.assert_array_equal(got.col[s:e], ref.col[s:e][o], err_msg=f"row {i}")
+        np.testing.assert_array_equal(bits(got.val[s:e]), bits(ref.val[s:e][o]), err_msg=f"row {i}")
+
+
+def _device_dia(A):
+    s = A.struct()
+    ha, da = ias.Dia(), ias.Dia()
+    ias.check(ias.lib.ias_csr_to_dia(C.byref(s), C.byref(ha), 0.0), "to_dia")
+    ias.check(ias.lib.ias_dia_copy(C.byref(ha), C.byref(da), ias.MEMORY_DEVICE, 0), "upload")
+    ias.lib.ias_dia_free(C.byref(ha))
+    return da
+
+
+def test_dia_into_rejects_aliased_c():
+    A = ias.gen_band(2048, 2, seed=3)
+    da = _device_dia(A)
+    try:
+        nd = C.c_int32(0)
+        ias.check(ias.lib.ias_dia_mul_dia_ndiag(C.byref(da), C.byref(da), C.byref(nd)), "ndiag")
+        assert nd.value == 9
+        # C = A in place: every array of C is one of A's
+        Ca = ias.Dia(rows=0, cols=0, num_diagonals=da.num_diagonals, choice=0,
+                     diagonal_offsets=da.diagonal_offsets, diagonal_ind=da.diagonal_ind, val=da.val,
+                     memory=ias.MEMORY_DEVICE, device=0)
+        assert ias.lib.ias_dia_mul_dia_into(C.byref(da), C.byref(da), C.byref(Ca), None, None) == 1
+        assert b"overlap" in ias.lib.ias_last_error()
+        # only the values overlap (C.val inside A's value array)
+        import torch
+        offs = torch.empty(nd.value, dtype=torch.int32, device="cuda:0")
+        ind = torch.empty(2 * 2048 - 1, dtype=torch.int32, device="cuda:0")
+        Cb = ias.Dia(rows=0, cols=0, num_diagonals=nd.value, choice=0,
+                     diagonal_offsets=C.cast(C.c_void_p(offs.data_ptr()), ias.i32p),
+                     diagonal_ind=C.cast(C.c_void_p(ind.data_ptr()), ias.i32p),
+                     val=C.cast(C.c_void_p(C.cast(da.val, C.c_void_p).value + 8 * 100), ias.f64p),
+                     memory=ias.MEMORY_DEVICE, device=0)
+        assert ias.lib.ias_dia_mul_dia_into(C.byref(da), C.byref(da), C.byref(Cb), None, None) == 1
+        # invalid operands of the ndiag query
+        bad = ias.Dia(rows=da.rows, cols=da.cols, num_diagonals=-1, choice=1, diagonal_offsets=da.diagonal_offsets,
+                      diagonal_ind=da.diagonal_ind, val=da.val, memory=ias.MEMORY_DEVICE, device=0)
+        assert ias.lib.ias_dia_mul_dia_ndiag(C.byref(bad), C.byref(da), C.byref(nd)) == 1
+        bad.num_diagonals, bad.choice = da.num_diagonals, 0
+        assert ias.lib.ias_dia_mul_dia_ndiag(C.byref(bad), C.byref(da), C.byref(nd)) == 8
+    finally:
+        ias.lib.ias_dia_free(C.byref(da))
+
+
+def test_block_cache_concurrent_threads():
+    """Four host threads, each with its own plan, multiply and free
+    library-allocated device outputs (block-cache sized) at once; every result
+    matches the oracle's nnz and value sum, so no thread got a block another
+    thread's kernels were still writing."""
+    mats = [ias.gen_rmat(12, 8, seed=s, value_mode=1) for s in (31, 32, 33, 34)]
+    refs = []
+    for A in mats:
+        r = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(A))
+        refs.append((r.nnz, float(r.val.sum())))
+    errors = []
+
+    def work(k):
+        try:
+            A = mats[k]
+            plan = C.c_void_p()
+            ias.check(ias.lib.ias_plan_create(C.byref(plan), 0, None), "plan")
+            s = A.struct()
+            o = ias.opts(output_memory=ias.MEMORY_DEVICE, device=0, plan=plan)
+            for it in range(25):
+                c = ias.Csr()
+                ias.check(ias.lib.ias_csr_mul_csr(C.byref(s), C.byref(s), C.byref(c), C.byref(o), None), "mul")
+                h = ias.Csr()
+                ias.check(ias.lib.ias_csr_copy(C.byref(c), C.byref(h), ias.MEMORY_HOST, 0), "download")
+                ias.lib.ias_csr_free(C.byref(c))
+                got = ias.csr_to_numpy(h)
+                if got.nnz != refs[k][0] or float(got.val.sum()) != refs[k][1]:
+                    errors.append((k, it, got.nnz, refs[k]))
+            ias.lib.ias_plan_destroy(plan)
+        except Exception as e:   # noqa: BLE001 — reported below
+            errors.append((k, repr(e)))
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:4]
