@@ -165,7 +165,12 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
         int32_t c[K];
         double bv[K];
         int32_t e[K];
-        uint32_t word[K], pre[K];   // the lane's bitmap word and its prefix count
+        // the step's 2K bitmap words (lanes 0 .. 2K-1) and their prefix counts
+        // (lanes 2K .. 4K-1): one load of 4K lanes instead of two 64-lane
+        // loads per window — the texture addresser, not HBM, bounds this pass
+        // (TA busy 90 % of its cycles, round 5), and every lane of those
+        // loads read one of two addresses
+        uint32_t wp;
     };
     // gathers of the step at window pw0.  Branch-free (clamped addresses for
     // the lanes and words outside the unit), so that the wait for a step's
@@ -181,15 +186,29 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
         for (int k = 0; k < K; ++k) {
             const int32_t pw = pw0 + 64 * k;
             const int32_t p = pw + lane;
-            const int ecur = __popcll(__ballot(bl > 0 && rel < pw));
-            S.e[k] = max(ecur + __popcll(wmask[w][k] & upto) - 1, 0);
+            const int ecur = (int)__popcll(__ballot(bl > 0 && rel < pw));
+            const int ei = ecur + (int)__popcll(wmask[w][k] & upto) - 1;
+            S.e[k] = ei > 0 ? ei : 0;
             const int64_t kb = (p >= pa && p < pb) ? ent[w][S.e[k]].bs + p : 0;
             S.c[k] = a.bcol[kb];
             S.bv[k] = a.bval[kb];
-            const int64_t wi = min(bmo + (pw >> 5) + (lane >> 5), lastw);
-            S.word[k] = a.bm.bits[wi];
-            S.pre[k] = a.bm.pref[wi];
         }
+        {
+            const int j = lane & (2 * K - 1);
+            const int64_t wi = min(bmo + (pw0 >> 5) + j, lastw);
+            const uint32_t *src = lane < 2 * K ? a.bm.bits : a.bm.pref;
+            S.wp = src[wi];
+        }
+    };
+    // window k's bitmap word and prefix for this lane (lanes 0-31: the
+    // window's first word, 32-63: its second)
+    auto words_of = [&](const Step &S, int k, uint32_t &word, uint32_t &pre) {
+        const uint32_t w0 = (uint32_t)__builtin_amdgcn_readlane((int)S.wp, 2 * k);
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_readlane((int)S.wp, 2 * k + 1);
+        const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)S.wp, 2 * K + 2 * k);
+        const uint32_t q1 = (uint32_t)__builtin_amdgcn_readlane((int)S.wp, 2 * K + 2 * k + 1);
+        word = lane < 32 ? w0 : w1;
+        pre = lane < 32 ? q0 : q1;
     };
     // stage the step's first touches by rank, park its duplicates, flush
     auto store = [&](int32_t pw0, const Step &S) {
@@ -197,7 +216,8 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int32_t p = pw0 + 64 * k + lane;
-            const uint32_t word = S.word[k], pre = S.pre[k];
+            uint32_t word, pre;
+            words_of(S, k, word, pre);
             const bool in = p >= pa && p < pb;
             const bool ft = in && ((word >> (lane & 31)) & 1u);
             const int32_t rk = (int32_t)(pre + (uint32_t)__popc(word & below));

@@ -2560,6 +2560,17 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     n_cols = cols;
     IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
+    // the previous call's symbolic bins are done: their durations for this
+    // call's balance, read while the analysis kernels run
+    for (int b = 0; b < MAX_BINS; ++b)
+        if (bin_rec[b]) {
+            bin_rec[b] = false;
+            float ms = 0.f;
+            if (sym_est_prev[b] > 0.0 && hipEventElapsedTime(&ms, bin_ev[2 * b], bin_ev[2 * b + 1]) == hipSuccess &&
+                ms > 0.f)
+                sym_w[b] = 1e6 * (double)ms / sym_est_prev[b];
+            (void)hipGetLastError();
+        }
     const BinSpec ss = sym_spec(sym_nval(cbm_path)), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
@@ -2631,7 +2642,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // left the two queues 0.55 ms apart on K3'); IAS_SYM_FEEDBACK=0: serial
     // weights only.
     int sym_lane[MAX_BINS] = {};
-    double sym_est[MAX_BINS] = {};
+    double *sym_est = sym_est_prev;   // read back with the bins' durations by the next call
+    std::fill(sym_est, sym_est + MAX_BINS, 0.0);
     const bool fb = !serial && !small && sym_feedback();
     if (fb && !bin_ev[0])
         for (auto &e : bin_ev) HIPC(hipEventCreate(&e));
@@ -2795,15 +2807,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     HIPC(hipEventRecord(ev[2], s));
     HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + nnz(C), unit counts
     HIPC((hipError_t)host_wait(s));
-    // the symbolic bins are done: their durations for the next call's balance
-    for (int b = 0; b < MAX_BINS; ++b)
-        if (bin_rec[b]) {
-            bin_rec[b] = false;
-            float ms = 0.f;
-            if (sym_est[b] > 0.0 && hipEventElapsedTime(&ms, bin_ev[2 * b], bin_ev[2 * b + 1]) == hipSuccess && ms > 0.f)
-                sym_w[b] = 1e6 * (double)ms / sym_est[b];
-            (void)hipGetLastError();
-        }
+    // the bins' durations are read by the next call, while its analysis runs
+    // (here they would delay the return by ~60 us of event queries)
     const Counters c2 = hc[1];
     nnz_total = rows > 0 ? (int64_t)c2.nnz_total : 0;
     n2_units = (int64_t)c2.n2_units;
@@ -2857,29 +2862,38 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     std::function<ias_status(hipStream_t, int)> launch_fix;   // part 0: sorted fix-ups, 1: the others, 2: all
     bool fix_split = false;
     int fix_lane = 0, n2_launches = 0, n2_mask = 0;
-    // big bins first: their long rows start early and the small bins fill in behind
+    // big bins first: their long rows start early and the small bins fill in
+    // behind.  The table bins (partitioned, wide, direct-write) take the first
+    // side streams and the streaming pass the next (at least the third), but
+    // the streaming pass — the phase's critical path — is launched first: the
+    // host issues ~30 API calls for the others (~60 us on K3')
     IAS_TRY(fork());
-    int lane_no = 0;
-    if (num_count[part_bin] > 0) {
-        hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, t>>>(
-            ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
-        CHECK_LAUNCH("k_numeric_part", t);
-    }
-    if ((c = num_count[wide_bin]) > 0) {
-        hipStream_t t = (hipStream_t)side_stream(lane_no++);
-        k_numeric_global<1024, 2, 256><<<c, 1024, 0, t>>>(ax, B, NL + st[wide_bin], as<int64_t>(bufs[B_WSOFF]),
-                                                          c, (char *)bufs[B_WS].p, out);
-        CHECK_LAUNCH("k_numeric_global", t);
-    }
-    for (int i = N_DW - 1; i >= 0; --i) {
-        const int b = ns.nval + 3 + i;
-        if ((c = num_count[b]) > 0) {
-            hipStream_t t = (hipStream_t)side_stream(lane_no++);
-            dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), t, ax, B, NL + st[b]}, out);
-            CHECK_LAUNCH("k_numeric_dw", t);
+    int lane_no = (num_count[part_bin] > 0 ? 1 : 0) + (num_count[wide_bin] > 0 ? 1 : 0);
+    for (int i = 0; i < N_DW; ++i) lane_no += num_count[ns.nval + 3 + i] > 0 ? 1 : 0;
+    auto launch_tables = [&]() -> ias_status {
+        int tl = 0;
+        if (num_count[part_bin] > 0) {
+            hipStream_t t = (hipStream_t)side_stream(tl++);
+            k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, t>>>(
+                ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
+            CHECK_LAUNCH("k_numeric_part", t);
         }
-    }
+        if ((c = num_count[wide_bin]) > 0) {
+            hipStream_t t = (hipStream_t)side_stream(tl++);
+            k_numeric_global<1024, 2, 256><<<c, 1024, 0, t>>>(ax, B, NL + st[wide_bin], as<int64_t>(bufs[B_WSOFF]),
+                                                              c, (char *)bufs[B_WS].p, out);
+            CHECK_LAUNCH("k_numeric_global", t);
+        }
+        for (int i = N_DW - 1; i >= 0; --i) {
+            const int b = ns.nval + 3 + i;
+            if ((c = num_count[b]) > 0) {
+                hipStream_t t = (hipStream_t)side_stream(tl++);
+                dw_bin(DW_BINS[i].cfg, Launch{c, slots_for(DW_BINS[i].upper), t, ax, B, NL + st[b]}, out);
+                CHECK_LAUNCH("k_numeric_dw", t);
+            }
+        }
+        return IAS_SUCCESS;
+    };
     // streaming rows: flat pass, then the duplicate fix-up (same stream, ordered).
     // Fixed lanes (side stream 2 for the pass, 3 for its fix-ups and the short
     // rows), whatever the bins before it: measured, the schedule is sensitive
@@ -2963,6 +2977,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         CHECK_LAUNCH("k_num2", t);
         if (!fix_split) IAS_TRY(launch_fix(t, 3));
     }
+    IAS_TRY(launch_tables());
     // short rows: all on the fix-up stream when the pass is split (ahead of
     // its waits; not behind the streaming pass on a shared queue)
     const int short_lane = fix_split ? fix_lane : -1;

@@ -118,6 +118,7 @@ struct ias_plan {
     // measured duration beside the others per estimated product (ns; 0: not
     // measured yet) and the events around its launches
     double sym_w[ias::MAX_BINS] = {};
+    double sym_est_prev[ias::MAX_BINS] = {};   // the last call's estimated products per bin
     hipEvent_t bin_ev[2 * ias::MAX_BINS] = {};
     bool bin_rec[ias::MAX_BINS] = {};
     unsigned long long num_ws = 0;

@@ -67,9 +67,12 @@ constexpr int S3_F1BPP = 32;   // f1 bits per product bound (false candidates ~ 
 template <int K>
 struct Sym3Lds {
     static constexpr int U = 64 * K;       // product bound
-    static constexpr int F1B = S3_F1BPP * U;   // f1 bits
+    // filter sizes rounded up to powers of two: the hashes' range reduction
+    // is then a shift, not a 64-bit multiply per product (K = 12, 24)
+    static constexpr int pow2(int x) { return x <= 1 ? 1 : 2 * pow2((x + 1) / 2); }
+    static constexpr int F1B = pow2(S3_F1BPP * U);   // f1 bits
     static constexpr int F1W = F1B / 32;
-    static constexpr int F2B = 2 * U;      // f2 bits
+    static constexpr int F2B = pow2(2 * U);      // f2 bits
     static constexpr int F2W = F2B / 32;   // >= 2K: its first words also hold the bitmap words (exact phase)
     static constexpr int NE = WAVE;        // A entries per row at most (one per lane)
     static constexpr int LC = U / 8;       // possible-duplicate list capacity
