@@ -33,7 +33,7 @@ namespace dev {
 template <int U, int F1BPP>
 struct Sym4Lds {
     static constexpr int NWIN = U / 64;            // 64-product windows
-    static constexpr int F1B = F1BPP * U;          // f1 bits
+    static constexpr int F1B = F1BPP * U;          // f1 bits (a power of two: 16 bits of hash)
     static constexpr int F1W = F1B / 32;
     static constexpr int F2B = 2 * U;              // f2 bits
     static constexpr int F2W = F2B / 32;
@@ -45,13 +45,13 @@ struct Sym4Lds {
     static constexpr int WPL = BW / WAVE;          // bitmap words per lane in the finish scan
     static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
     static_assert(BW % WAVE == 0 && LC % WAVE == 0 && NE % WAVE == 0, "whole waves");
+    static_assert(NWIN <= WAVE, "one window base per lane");
+    static_assert(F1B == 65536 && F2B <= F1B / 8, "f1 indexed by 16 hash bits, f2 by their top bits");
     __attribute__((aligned(16))) uint32_t f1[F1W];
     __attribute__((aligned(16))) uint32_t f2[F2W];
     unsigned long long smask[NWIN];                // entry start bits per window
-    union {
-        unsigned long long cand[NWIN];             // candidate bits per window (filter, classify)
-        uint32_t pref[BW];                         // exclusive prefixes of the bitmap words (finish)
-    };
+    int32_t wbase[NWIN];                           // non-empty entries starting before each window
+    uint32_t pref[BW];                             // exclusive prefixes of the bitmap words (finish)
     int32_t ebase[NE];                             // B-row start - first product, per non-empty entry
     uint32_t words[BW];                            // first-touch bitmap
     __device__ int2 *list() { return (int2 *)f1; }
@@ -59,10 +59,19 @@ struct Sym4Lds {
     __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
 };
 
-constexpr int SYM4_WPE = 4;   // waves per SIMD the registers must allow (LDS allows 3.5 at U = 4096)
+// 16 bits of a column's multiplicative hash: f1's bit index; f2's is its top
+// log2(F2B) bits (a coarsening: a column's products share both, which is all
+// the filter's exactness needs).
+__device__ __forceinline__ uint32_t s4_hash16(int32_t c) { return ((uint32_t)c * 0x9E3779B1u) >> 16; }
+
+constexpr int SYM4_WPE = 3;   // waves per SIMD the registers must allow (LDS allows 3.5 at U = 4096)
 template <int U, int F1BPP, int KC, int WPB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_WPE))) void k_sym4(Sym3Args) {
     using LDS = Sym4Lds<U, F1BPP>;
+    constexpr int NWIN = LDS::NWIN;
+    constexpr int NCH = NWIN / KC;                 // chunks of KC windows
+    static_assert(NWIN % KC == 0 && NWIN % 2 == 0, "whole chunks");
+    constexpr int F2SH = 16 - ilog2(LDS::F2B);      // f2 bit = hash16 >> F2SH
     __shared__ LDS lds[WPB];
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)__lane_id();
@@ -113,7 +122,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         }
         const int64_t q0 = ref.q0;
         const int nwin = (P + 63) >> 6;
-        for (int k = lane; k < nwin; k += WAVE) L.smask[k] = 0ull;
+        if (lane < NWIN) L.smask[lane] = 0ull;
         s3_sync();
         // ---- stage the entries, 64 at a time
         {
@@ -142,98 +151,94 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
             }
         }
         s3_sync();
-        // columns of windows k0 .. k0+KC-1 (c0: non-empty entries starting
-        // before window k0, advanced past the chunk).  Windows beyond the row
-        // and lanes beyond P read B.col[0] (callers mask them): branch-free, so
-        // the wait for a chunk's loads counts exactly the loads issued after it.
+        // window bases: lane k holds window k's
+        {
+            const int cnt = lane < nwin ? (int)__popcll(L.smask[lane]) : 0;
+            if (lane < NWIN) L.wbase[lane] = wave_incl_sum(cnt) - cnt;
+        }
+        s3_sync();
+        // product p = 64k + lane: its entry and B column (beyond P: B.col[0],
+        // callers mask it)
         const char *base = (const char *)s3_args()->bcol;
-        auto gather = [&](int k0, int32_t(&c)[KC], int &c0) {
-            int32_t eb[KC];
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const uint64_t m = L.smask[min(k0 + t, LDS::NWIN - 1)];
-                const bool inw = k0 + t < nwin;
-                const int e = min(max(c0 + (int)__popcll(m & upto) - 1, 0), LDS::NE - 1);
-                eb[t] = L.ebase[e];
-                c0 += inw ? (int)__popcll(m) : 0;
-            }
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const int p = 64 * (k0 + t) + lane;
-                const uint32_t off = p < P ? (uint32_t)(eb[t] + p) << 2 : 0u;
-                c[t] = *(const int32_t *)(base + off);
-            }
+        auto col_addr = [&](int k, int l) -> uint32_t {
+            const int kk = min(k, NWIN - 1);
+            const uint64_t m = L.smask[kk];
+            const int e = min(max(L.wbase[kk] + (int)__popcll(m & ((2ull << l) - 1ull)) - 1, 0), LDS::NE - 1);
+            return l < P - 64 * k ? (uint32_t)(L.ebase[e] + 64 * k + l) << 2 : 0u;
         };
-        // two chunk buffers: chunk j+1's gathers fly while chunk j is worked on
-        auto sweep = [&](auto &&work) {
-            int c0 = 0;
-            int32_t ca[KC], cb[KC];
-            gather(0, ca, c0);
-            for (int k0 = 0; k0 < nwin; k0 += 2 * KC) {
-                gather(k0 + KC, cb, c0);
-                work(k0, ca);
-                if (k0 + KC >= nwin) break;
-                gather(k0 + 2 * KC, ca, c0);
-                work(k0 + KC, cb);
-            }
+        auto gather = [&](int k0, int32_t(&c)[KC]) {
+            uint32_t off[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) off[t] = col_addr(k0 + t, lane);
+#pragma unroll
+            for (int t = 0; t < KC; ++t) c[t] = *(const int32_t *)(base + off[t]);
         };
         tm.mark(0);
-        // ---- filter pass
-        sweep([&](int k0, const int32_t(&c)[KC]) {
-            uint32_t old[KC], bit[KC];
+        // ---- filter: one sweep; each product's 16 hash bits stay in the
+        // lanes (two per register) with its candidate bit, so the classify
+        // pass needs no second gather of the row's columns
+        uint32_t hh2[NWIN / 2];
+        uint64_t candm = 0ull;
+        {
+            int32_t ca[KC], cb[KC];
+            gather(0, ca);
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool in = 64 * (k0 + t) + lane < P;
-                const uint32_t h = s3_h1(c[t], LDS::F1B);
-                bit[t] = in ? 1u << (h & 31) : 0u;
-                uint32_t o = 0u;   // lanes / windows past the row issue nothing
-                if (in) o = atomicOr(&L.f1[h >> 5], bit[t]);
-                old[t] = o;
-            }
+            for (int j = 0; j < NCH; ++j) {
+                int32_t(&c)[KC] = (j & 1) ? cb : ca;
+                int32_t(&nx)[KC] = (j & 1) ? ca : cb;
+                if (j + 1 < NCH && KC * (j + 1) < nwin) gather(KC * (j + 1), nx);
+                if (KC * j >= nwin) continue;   // beyond the row: nothing to filter
+                uint32_t hv[KC], old[KC], bit[KC];
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool cand = (old[t] & bit[t]) != 0u;
-                if (cand) {
-                    const uint32_t h = s3_h2(c[t], LDS::F2B);
-                    atomicOr(&L.f2[h >> 5], 1u << (h & 31));
+                for (int t = 0; t < KC; ++t) {
+                    const int k = KC * j + t;
+                    const bool in = lane < P - 64 * k;
+                    hv[t] = s4_hash16(c[t]);
+                    bit[t] = in ? 1u << (hv[t] & 31) : 0u;
+                    uint32_t o = 0u;   // lanes / windows past the row issue nothing
+                    if (in) o = atomicOr(&L.f1[hv[t] >> 5], bit[t]);
+                    old[t] = o;
                 }
-                const uint64_t cb = __ballot(cand);
-                if (lane == 0 && k0 + t < nwin) L.cand[k0 + t] = cb;
+#pragma unroll
+                for (int t = 0; t < KC; ++t) {
+                    const int k = KC * j + t;
+                    const bool cand = (old[t] & bit[t]) != 0u;
+                    candm |= (cand ? 1ull : 0ull) << k;
+                    if (cand) {
+                        const uint32_t h2 = hv[t] >> F2SH;
+                        atomicOr(&L.f2[h2 >> 5], 1u << (h2 & 31));
+                    }
+                    if (t & 1) hh2[k >> 1] = (hv[t] << 16) | hv[t - 1];
+                }
             }
-        });
+        }
         // the next row's details fly during the rest of this one
         const Det nxt = details(nref);
         tm.mark(1);
         s3_sync();   // f1 dead from here: the list overlays it
-        // ---- classify pass: certain first touches -> bitmap words, possible
-        // duplicates -> list (product order)
+        // ---- classify: certain first touches -> bitmap words, possible
+        // duplicates -> list (product order; their columns gathered after)
         int nl = 0;
         int2 *list = L.list();
-        sweep([&](int k0, const int32_t(&c)[KC]) {
-            uint32_t f2w[KC];
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool in = 64 * (k0 + t) + lane < P;
-                f2w[t] = L.f2[in ? s3_h2(c[t], LDS::F2B) >> 5 : 0u];
-            }
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const int k = k0 + t;
+        for (int k = 0; k < NWIN; ++k) {
+            if (k < nwin) {
                 const int p = 64 * k + lane;
-                const bool in = p < P;
-                const uint64_t cm = L.cand[min(k, LDS::NWIN - 1)];
-                const bool poss =
-                    in && (((cm >> lane) & 1ull) || ((f2w[t] >> (s3_h2(c[t], LDS::F2B) & 31)) & 1u));
+                const bool in = lane < P - 64 * k;
+                const uint32_t hv = (hh2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                const uint32_t h2 = hv >> F2SH;
+                const uint32_t f2w = L.f2[in ? h2 >> 5 : 0u];
+                const bool poss = in && (((candm >> k) & 1ull) || ((f2w >> (h2 & 31)) & 1u));
                 const uint64_t b = __ballot(in && !poss);
-                if (lane == 0 && k < nwin) *(uint64_t *)&L.words[2 * k] = b;
+                if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
                 const uint64_t pb = __ballot(poss);
                 if (poss) {
                     const int i = nl + (int)__popcll(pb & lt);
-                    if (i < LDS::LC) list[i] = make_int2(c[t], p);
+                    if (i < LDS::LC) list[i] = make_int2(0, p);
                 }
                 nl += (int)__popcll(pb);
             }
-        });
+        }
         s3_sync();
         tm.mark(2);
         const bool retry = 4 * nl > 3 * LDS::LC;
@@ -243,16 +248,27 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 s3_args()->retry[j] = ref;
             }
         } else {
-            // ---- exact: claim the column (CAS, linear probing); its smallest
-            // product is the first touch
+            // ---- exact: the listed products' columns (gathered again, only
+            // these), then claim the column (CAS, linear probing); its
+            // smallest product is the first touch
             int2 e[LDS::LT];
             uint32_t slot[LDS::LT], f[LDS::LT];
+            uint32_t off[LDS::LT];
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t) {
                 e[t] = make_int2(0, -1);
                 slot[t] = 0;
                 f[t] = 0;
+                off[t] = 0u;
+                const int i = t * WAVE + lane;
+                if (i < nl) {
+                    e[t].y = list[i].y;
+                    off[t] = col_addr(e[t].y >> 6, e[t].y & 63);
+                }
             }
+#pragma unroll
+            for (int t = 0; t < LDS::LT; ++t)
+                if (t * WAVE + lane < nl) e[t].x = *(const int32_t *)(base + off[t]);
             if (nl > 0) {
                 int32_t *keys = L.keys();
                 uint32_t *own = L.own();
@@ -263,7 +279,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 for (int t = 0; t < LDS::LT; ++t) {
                     const int i = t * WAVE + lane;
                     if (i < nl) {
-                        e[t] = list[i];
                         uint32_t s = s3_h3(e[t].x, LDS::ES);
                         bool won = false;
                         for (int probe = 0; probe < LDS::ES; ++probe) {

@@ -40,34 +40,36 @@ struct Sym5Lds {
     static constexpr int WIN_PL = NWIN / WAVE;     // windows per lane in wave 0's window scan
     static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
     static_assert(LC % T == 0 && BW % T == 0 && NWIN % WAVE == 0, "whole workgroups");
+    static_assert(F2B <= 65536, "f2 index in 16 bits");
     __attribute__((aligned(16))) uint32_t f1[F1W];
     __attribute__((aligned(16))) uint32_t f2[F2W];
     unsigned long long smask[NWIN];                // entry start bits per window
-    union {
-        unsigned long long cand[NWIN];             // candidate bits per window
-        uint32_t pref[BW];                         // word prefixes (finish)
-    };
+    uint32_t pref[BW];                             // word prefixes (finish)
     int32_t cbase[NWIN];                           // non-empty entries starting before each window
     int32_t ebase[NE];
     uint32_t words[BW];
     int32_t nl;                                    // list counter
     int32_t scratch[NW];
-    __device__ int2 *list() { return (int2 *)f1; }
+    __device__ int32_t *list() { return (int32_t *)f1; }
     __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
     __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
 };
 
 template <int U, int NW, int KC>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void k_sym5(Sym3Args) {
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) void k_sym5(Sym3Args) {
     using LDS = Sym5Lds<U, NW>;
     using TM = Team<LDS::T>;
     constexpr int T = LDS::T;
+    constexpr int WWIN = LDS::NWIN / NW;           // windows per wave
+    constexpr int NCH = WWIN / KC;                 // its chunks of KC windows
+    static_assert(WWIN <= WAVE && WWIN % KC == 0 && KC % 2 == 0, "a wave's windows: one candidate mask");
+    constexpr int SH1 = 32 - ilog2(LDS::F1B);      // f1 bit = hash >> SH1
+    constexpr int SH2 = 32 - ilog2(LDS::F2B);      // f2 bit = hash >> SH2 (f1's top bits)
     __shared__ LDS L;
     const int tid = (int)threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int lane = (int)__lane_id();
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t upto = (2ull << lane) - 1ull;
     for (int i = tid; i < LDS::F1W / 4; i += T) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = tid; i < LDS::F2W; i += T) L.f2[i] = 0u;
 
@@ -128,90 +130,89 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
             }
         }
         __syncthreads();
+        // product p = 64k + l: the byte offset of its B column (beyond P:
+        // B.col[0], callers mask it)
         const char *base = (const char *)s3_args()->bcol;
-        auto gather = [&](int k0, int32_t(&c)[KC]) {
-            int32_t eb[KC];
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const int k = min(k0 + t, LDS::NWIN - 1);
-                const uint64_t m = L.smask[k];
-                const int e = min(max(L.cbase[k] + (int)__popcll(m & upto) - 1, 0), LDS::NE - 1);
-                eb[t] = L.ebase[e];
-            }
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const int p = 64 * (k0 + t) + lane;
-                const uint32_t off = p < P ? (uint32_t)(eb[t] + p) << 2 : 0u;
-                c[t] = *(const int32_t *)(base + off);
-            }
+        auto col_addr = [&](int k, int l) -> uint32_t {
+            const int kk = min(k, LDS::NWIN - 1);
+            const uint64_t m = L.smask[kk];
+            const int e = min(max(L.cbase[kk] + (int)__popcll(m & ((2ull << l) - 1ull)) - 1, 0), LDS::NE - 1);
+            return l < P - 64 * k ? (uint32_t)(L.ebase[e] + 64 * k + l) << 2 : 0u;
         };
-        // this wave's chunks w, w + NW, ... of KC windows; two buffers
-        auto sweep = [&](auto &&work) {
-            constexpr int STEP = NW * KC;
+        // this wave's chunk j: windows w*KC + j*NW*KC .. +KC (wr: w, opaque
+        // per row, so the per-window bounds are not all hoisted out of the row
+        // loop into registers that then spill)
+        int wr = w;
+        asm volatile("" : "+s"(wr));
+        auto gather = [&](int j, int32_t(&c)[KC]) {
+            const int k0 = (wr + j * NW) * KC;
+            uint32_t off[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) off[t] = col_addr(k0 + t, lane);
+#pragma unroll
+            for (int t = 0; t < KC; ++t) c[t] = *(const int32_t *)(base + off[t]);
+        };
+        // ---- filter: one sweep; each product's f2 index stays in the lanes
+        // (two per register) with its candidate bit, so classify gathers nothing
+        uint32_t hh2[WWIN / 2];
+        uint64_t candm = 0ull;
+        {
             int32_t ca[KC], cb[KC];
-            int k0 = w * KC;
-            gather(k0, ca);
-            for (; k0 < nwin; k0 += 2 * STEP) {
-                gather(k0 + STEP, cb);
-                work(k0, ca);
-                if (k0 + STEP >= nwin) break;
-                gather(k0 + 2 * STEP, ca);
-                work(k0 + STEP, cb);
-            }
-        };
-        // ---- filter
-        sweep([&](int k0, const int32_t(&c)[KC]) {
-            uint32_t old[KC], bit[KC];
+            gather(0, ca);
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool in = 64 * (k0 + t) + lane < P;
-                const uint32_t h = s3_h1(c[t], LDS::F1B);
-                bit[t] = in ? 1u << (h & 31) : 0u;
-                uint32_t o = 0u;   // lanes / windows past the row issue nothing
-                if (in) o = atomicOr(&L.f1[h >> 5], bit[t]);
-                old[t] = o;
-            }
+            for (int j = 0; j < NCH; ++j) {
+                int32_t(&c)[KC] = (j & 1) ? cb : ca;
+                int32_t(&nx)[KC] = (j & 1) ? ca : cb;
+                const int k0 = (wr + j * NW) * KC;
+                if (j + 1 < NCH && k0 + NW * KC < nwin) gather(j + 1, nx);
+                if (k0 >= nwin) continue;   // beyond the row: nothing to filter
+                uint32_t hv[KC], old[KC], bit[KC];
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool cand = (old[t] & bit[t]) != 0u;
-                if (cand) {
-                    const uint32_t h = s3_h2(c[t], LDS::F2B);
-                    atomicOr(&L.f2[h >> 5], 1u << (h & 31));
+                for (int t = 0; t < KC; ++t) {
+                    const bool in = lane < P - 64 * (k0 + t);
+                    hv[t] = (uint32_t)c[t] * 0x9E3779B1u;
+                    const uint32_t h1 = hv[t] >> SH1;
+                    bit[t] = in ? 1u << (h1 & 31) : 0u;
+                    uint32_t o = 0u;   // lanes / windows past the row issue nothing
+                    if (in) o = atomicOr(&L.f1[h1 >> 5], bit[t]);
+                    old[t] = o;
                 }
-                const uint64_t cb = __ballot(cand);
-                if (lane == 0 && k0 + t < nwin) L.cand[k0 + t] = cb;
+#pragma unroll
+                for (int t = 0; t < KC; ++t) {
+                    const int lk = KC * j + t;
+                    const bool cand = (old[t] & bit[t]) != 0u;
+                    candm |= (cand ? 1ull : 0ull) << lk;
+                    const uint32_t h2 = hv[t] >> SH2;
+                    if (cand) atomicOr(&L.f2[h2 >> 5], 1u << (h2 & 31));
+                    if (t & 1) hh2[lk >> 1] = (h2 << 16) | (hv[t - 1] >> SH2);
+                }
             }
-        });
+        }
         __syncthreads();   // f1 dead: the list overlays it
-        // ---- classify
-        int2 *list = L.list();
-        sweep([&](int k0, const int32_t(&c)[KC]) {
-            uint32_t f2w[KC];
+        // ---- classify: certain first touches -> bitmap words, possible
+        // duplicates -> list (any order; their columns gathered after)
+        int32_t *list = L.list();
 #pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const bool in = 64 * (k0 + t) + lane < P;
-                f2w[t] = L.f2[in ? s3_h2(c[t], LDS::F2B) >> 5 : 0u];
-            }
-#pragma unroll
-            for (int t = 0; t < KC; ++t) {
-                const int k = k0 + t;
+        for (int lk = 0; lk < WWIN; ++lk) {
+            const int k = (wr + (lk / KC) * NW) * KC + lk % KC;
+            if (k < nwin) {
                 const int p = 64 * k + lane;
-                const bool in = p < P;
-                const uint64_t cm = L.cand[min(k, LDS::NWIN - 1)];
-                const bool poss =
-                    in && (((cm >> lane) & 1ull) || ((f2w[t] >> (s3_h2(c[t], LDS::F2B) & 31)) & 1u));
+                const bool in = lane < P - 64 * k;
+                const uint32_t h2 = (hh2[lk >> 1] >> (16 * (lk & 1))) & 0xFFFFu;
+                const uint32_t f2w = L.f2[in ? h2 >> 5 : 0u];
+                const bool poss = in && (((candm >> lk) & 1ull) || ((f2w >> (h2 & 31)) & 1u));
                 const uint64_t b = __ballot(in && !poss);
-                if (lane == 0 && k < nwin) *(uint64_t *)&L.words[2 * k] = b;
+                if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
                 const uint64_t pb = __ballot(poss);
                 if (pb) {
                     int at = 0;
                     if (lane == 0) at = atomicAdd(&L.nl, (int)__popcll(pb));
                     at = __shfl(at, 0);
                     const int i = at + (int)__popcll(pb & lt);
-                    if (poss && i < LDS::LC) list[i] = make_int2(c[t], p);
+                    if (poss && i < LDS::LC) list[i] = p;
                 }
             }
-        });
+        }
         __syncthreads();
         const int32_t nl = L.nl;
         if (4 * nl > 3 * LDS::LC) {
@@ -220,14 +221,26 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
                 s3_args()->retry[j] = ref;
             }
         } else {
+            // ---- exact: the listed products' columns (gathered again, only
+            // these), then claim the column (CAS, linear probing); its
+            // smallest product is the first touch
             int2 e[LDS::LT];
-            uint32_t slot[LDS::LT], f[LDS::LT];
+            uint32_t slot[LDS::LT], f[LDS::LT], off[LDS::LT];
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t) {
                 e[t] = make_int2(0, -1);
                 slot[t] = 0;
                 f[t] = 0;
+                off[t] = 0u;
+                const int i = t * T + tid;
+                if (i < nl) {
+                    e[t].y = list[i];
+                    off[t] = col_addr(e[t].y >> 6, e[t].y & 63);
+                }
             }
+#pragma unroll
+            for (int t = 0; t < LDS::LT; ++t)
+                if (t * T + tid < nl) e[t].x = *(const int32_t *)(base + off[t]);
             if (nl > 0) {
                 int32_t *keys = L.keys();
                 uint32_t *own = L.own();
@@ -238,7 +251,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) vo
                 for (int t = 0; t < LDS::LT; ++t) {
                     const int i = t * T + tid;
                     if (i < nl) {
-                        e[t] = list[i];
                         uint32_t s = s3_h3(e[t].x, LDS::ES);
                         bool won = false;
                         for (int probe = 0; probe < LDS::ES; ++probe) {
