@@ -1978,6 +1978,20 @@ constexpr int32_t WIDE_MIN = (1 << 19) - 1;
 // noise on K3': 9.63 / 9.60 / 9.61 ms, profiles/r04/ab/cbm_cost_ab.txt)
 constexpr double CBM_COST = 20.0;
 // IAS_SYM_CBM=0: the partitioned rows take the hash partitions (A/B)
+static bool retry_print() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_RETRY_PRINT");
+        return e && *e == '1';
+    }();
+    return on;
+}
+static bool retry_feedback() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_RETRY_FEEDBACK");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
 static bool sym_feedback() {
     static const bool on = [] {
         const char *e = getenv("IAS_SYM_FEEDBACK");
@@ -2237,19 +2251,14 @@ static void sym3_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM3_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM3_WPB, 0, s>>>(a);
 }
-// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX), then sym2's 128-lane teams over
-// the rows it handed back (count read on the device)
-static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
+// a sym3 bin (upper in SYM3_MIN .. SYM3_MAX); the rows it hands back go to
+// sym2's 128- / 256-lane teams (retry_cfg, launched by the caller)
+static void sym3_bin(int32_t upper, const Sym3Args &a, hipStream_t s) {
     if (upper <= 512) sym3_launch<8>(a, s);
     else if (upper <= 768) sym3_launch<12>(a, s);
     else if (upper <= 1024) sym3_launch<16>(a, s);
     else if (upper <= 1536) sym3_launch<24>(a, s);
     else sym3_launch<32>(a, s);
-    retry.list = a.retry;
-    retry.count = a.count;   // grid bound; the device count decides
-    retry.count_dev = a.retry_count;
-    if (upper <= 1024) sym2_launch<128, 8, 1, SYM2_WPE_TEAM>(retry, s);
-    else sym2_launch<256, 8, 1, SYM2_WPE_TEAM>(retry, s);
 }
 
 // sym4's one-wave long rows (sym4_kernels.hpp): rows of SYM3_MAX+1 .. SYM4_MAX
@@ -2258,18 +2267,13 @@ static void sym3_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream
 // 4,097 - 8,192 1.0 ms (sym2's 1024-lane teams 0.96 ms: kept).
 constexpr int32_t SYM4_MAX = 4096;
 constexpr int SYM4_WPB = 2;
+// (its retries: sym2's 512-lane teams, cfg 6)
 template <int U>
 static void sym4_launch(const Sym3Args &a, hipStream_t s) {
     auto kern = k_sym4<U, 16, 8, SYM4_WPB>;
     const int64_t want = ((int64_t)a.count + SYM4_WPB - 1) / SYM4_WPB;
     const int64_t grid = std::min<int64_t>(want, resident_blocks(kern, 64 * SYM4_WPB, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * SYM4_WPB, 0, s>>>(a);
-}
-static void sym4_bin(const Sym3Args &a, Sym2Args retry, hipStream_t s) {
-    retry.list = a.retry;
-    retry.count_dev = a.retry_count;   // retry.count (the bin's rows) bounds the grid
-    sym4_launch<SYM4_MAX>(a, s);
-    sym2_launch<512, 8, 1, SYM2_WPE_TEAM>(retry, s);   // the 2,049 - 4,096 bins' team (cfg 6)
 }
 
 // sym5 (sym5_kernels.hpp): SYM4_MAX+1 .. SYM5_MAX products, NW waves per row
@@ -2280,16 +2284,10 @@ static void sym5_launch(const Sym3Args &a, hipStream_t s) {
     const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
     kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
 }
-static void sym5_bin(int32_t upper, const Sym3Args &a, Sym2Args retry, hipStream_t s) {
-    retry.list = a.retry;
-    retry.count_dev = a.retry_count;
-    if (upper <= 8192) {
-        sym5_launch<8192, 2>(a, s);
-        sym2_launch<1024, 8, 1, SYM2_WPE_TEAM>(retry, s);    // the bins' team (cfg 7)
-    } else {
-        sym5_launch<16384, 4>(a, s);
-        sym2_launch<1024, 16, 1, SYM2_WPE_TEAM>(retry, s);   // SYM2_CFG_WIDE
-    }
+// (its retries: sym2's 1024-lane teams, cfg 7 / SYM2_CFG_WIDE)
+static void sym5_bin(int32_t upper, const Sym3Args &a, hipStream_t s) {
+    if (upper <= 8192) sym5_launch<8192, 2>(a, s);
+    else sym5_launch<16384, 4>(a, s);
 }
 
 template <int TEAM, int K, int SEG, int TPW, int PER>
@@ -2712,6 +2710,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         }
         bin_mark(sym_part, t, 1);
     }
+    // The rows a sym3 / sym4 / sym5 bin hands back (list overflow, too many
+    // entries) are finished by sym2's teams, launched right after the bin in
+    // its stream (launched after the join instead, on the main stream, they
+    // ran last and serially: K3' symbolic +0.1 - 0.25 ms, rounds 4 and 5)
+    auto retry = [&](int cfg, const Sym3Args &a3, Sym2Args r2, hipStream_t t) {
+        r2.list = a3.retry;
+        r2.count_dev = a3.retry_count;   // r2.count bounds the grid; the device count decides
+        sym2_bin(cfg, r2, t);
+    };
     auto launch_sym = [&](int b, int c, hipStream_t t) -> ias_status {
         const int32_t u = SYM2_BINS[b - 1].upper;
         if (u <= SHORT_MAX) {
@@ -2722,11 +2729,22 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         }
         Sym2Args a2{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), sym2_layout(u, SYM2_BINS[b - 1].cfg), nnz, bm,
                     sa.dup_off, sa.dupn, sa.dupt, dcap_for(u), DW_MAX, nullptr};
+        // the retry teams' grid (persistent: any grid finishes the list): a
+        // bin hands back few rows, and a full grid of LDS-heavy workgroups
+        // waits for whole CUs beside the other bins (K3': 50 - 260 us per
+        // retry launch for ~no rows) — so twice the rows this bin handed back
+        // on the plan's last call, when known (IAS_RETRY_FEEDBACK=0: the bin's
+        // rows)
+        retry_upper_cur[b & 15] = u;
+        Sym2Args r2 = a2;
+        if (retry_feedback() && retry_prev[b & 15] >= 0 && retry_upper[b & 15] == u)
+            r2.count = std::min<int32_t>(c, 2 * retry_prev[b & 15] + 2);
         if (!c1.wide_b && u > SYM4_MAX && u <= SYM5_MAX) {
             const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                               sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                               &dc->s3_retry[b & 15]};
-            sym5_bin(u, a5, a2, t);
+            sym5_bin(u, a5, t);
+            retry(SYM2_BINS[b - 1].cfg, a5, r2, t);
             CHECK_LAUNCH("k_sym5", t);
             return IAS_SUCCESS;
         }
@@ -2734,7 +2752,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             const Sym3Args a4{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                               sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                               &dc->s3_retry[b & 15]};
-            sym4_bin(a4, a2, t);
+            sym4_launch<SYM4_MAX>(a4, t);
+            retry(SYM2_BINS[b - 1].cfg, a4, r2, t);
             CHECK_LAUNCH("k_sym4", t);
             return IAS_SUCCESS;
         }
@@ -2742,9 +2761,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             const Sym3Args a3{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                               sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                               &dc->s3_retry[b & 15]};   // a counter per bin (bins run concurrently)
-            Sym2Args r2 = a2;
             r2.lay = sym2_layout(u, u <= 1024 ? 4 : 5);   // the 128- / 256-lane team layout of this bound
-            sym3_bin(u, a3, r2, t);
+            sym3_bin(u, a3, t);
+            retry(u <= 1024 ? 4 : 5, a3, r2, t);
             CHECK_LAUNCH("k_sym3", t);
             return IAS_SUCCESS;
         }
@@ -2805,8 +2824,14 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     }
     HIPC(hipGetLastError());
     HIPC(hipEventRecord(ev[2], s));
-    HIPC(hipMemcpyAsync(hc + 1, dc2, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + nnz(C), unit counts
+    // both counter sets: [1] nnz(C), unit counts; [0] the bins' retry counts
+    HIPC(hipMemcpyAsync(hc, dc, 2 * sizeof(Counters), hipMemcpyDeviceToHost, s));
     HIPC((hipError_t)host_wait(s));
+    for (int i = 0; i < 16; ++i) retry_prev[i] = c1.wide_b ? -1 : hc[0].s3_retry[i];
+    std::copy(retry_upper_cur, retry_upper_cur + 16, retry_upper);
+    if (retry_print())   // IAS_RETRY_PRINT=1: rows each bin handed to sym2 (stderr)
+        for (int i = 0; i < 16; ++i)
+            if (retry_upper[i] > 0) fprintf(stderr, "ias retry: bin <= %d products: %d rows\n", retry_upper[i], retry_prev[i]);
     // the bins' durations are read by the next call, while its analysis runs
     // (here they would delay the return by ~60 us of event queries)
     const Counters c2 = hc[1];

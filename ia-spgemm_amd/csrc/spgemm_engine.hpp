@@ -119,6 +119,11 @@ struct ias_plan {
     // measured yet) and the events around its launches
     double sym_w[ias::MAX_BINS] = {};
     double sym_est_prev[ias::MAX_BINS] = {};   // the last call's estimated products per bin
+    // rows each sym3 / sym4 / sym5 bin handed to sym2 on the last call (-1:
+    // unknown): this call's retry grids are sized from them
+    int32_t retry_prev[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    int32_t retry_upper[16] = {};       // the product bound of the bin each count belongs to
+    int32_t retry_upper_cur[16] = {};   //   (this call's, until its counts are read)
     hipEvent_t bin_ev[2 * ias::MAX_BINS] = {};
     bool bin_rec[ias::MAX_BINS] = {};
     unsigned long long num_ws = 0;

@@ -10,16 +10,18 @@
 // sym3 (sym3_kernels.hpp) keeps a row's columns in registers (K per lane) and
 // its entries one per lane, so it stops at 2,048 products (K = 32: 168 VGPRs,
 // 3 waves per SIMD).  Here the columns never stay in registers beyond a chunk:
-//   * the row's entries (up to U/16) are staged in groups of 64 — per entry
-//     its B-row base in LDS and its start bit in the per-window start masks;
-//   * filter pass (per chunk: gather, f1 ORs with return, candidates mark
-//     f2; the chunk's candidate bits go to LDS as one ballot per window);
-//   * classify pass (per chunk: the same gathers again — the row's columns
-//     are L2 / Infinity-Cache resident by then — f2 reads, one ballot per
-//     window gives the certain first touches, the possible duplicates are
-//     listed over the dead f1);
-//   * exact pass over the list and finish as in sym3, with the bitmap words
-//     and their prefixes in LDS.
+//   * the row's entries (up to U/32) are staged in groups of 64 — per entry
+//     its B-row base in LDS and its start bit in the per-window start masks —
+//     and each window's count of entries starting before it (one per lane);
+//   * filter (per chunk of KC windows, double-buffered gathers: f1 ORs with
+//     return, candidates mark f2).  Each product's f2 index (16 bits, an
+//     independent hash) stays in the lanes, two per register, with its
+//     candidate bit: the row's columns are gathered once;
+//   * classify (registers + f2 reads): one ballot per window gives the
+//     certain first touches, the possible duplicates' product indices are
+//     listed over the dead f1;
+//   * exact pass: the listed products' columns gathered again (only those),
+//     then as in sym3, with the bitmap words and their prefixes in LDS.
 // Rows beyond the kernel's bounds, or whose list overflows, go to the retry
 // list that sym2's teams finish.  Measured against sym2's 512 / 1024-lane
 // teams on K3': see DESIGN.md §4.
@@ -39,14 +41,18 @@ struct Sym4Lds {
     static constexpr int F2W = F2B / 32;
     static constexpr int BW = U / 32;              // bitmap words
     static constexpr int NE = U / 32;              // A entries per row at most
-    static constexpr int LC = U * F1BPP / 128;     // possible-duplicate list (8 B each) +
-    static constexpr int ES = LC;                  //   exact table (8 B per slot) = f1's bytes
+    // possible-duplicate list (a product index, 4 B each) + exact table (8 B
+    // per slot) over f1: 12 B per entry, whole waves (U / 6.4 at F1BPP = 16;
+    // U / 8 with 8-byte entries left 17 % of K3''s 4,097 - 8,192-product rows
+    // to sym2)
+    static constexpr int LC = F1W / 3 / WAVE * WAVE;
+    static constexpr int ES = LC;
     static constexpr int LT = LC / WAVE;           // list entries per lane
     static constexpr int WPL = BW / WAVE;          // bitmap words per lane in the finish scan
-    static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
+    static_assert(4 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
     static_assert(BW % WAVE == 0 && LC % WAVE == 0 && NE % WAVE == 0, "whole waves");
     static_assert(NWIN <= WAVE, "one window base per lane");
-    static_assert(F1B == 65536 && F2B <= F1B / 8, "f1 indexed by 16 hash bits, f2 by their top bits");
+    static_assert(F1B == 65536 && F2B <= 65536, "f1 and f2 indexed by at most 16 hash bits");
     __attribute__((aligned(16))) uint32_t f1[F1W];
     __attribute__((aligned(16))) uint32_t f2[F2W];
     unsigned long long smask[NWIN];                // entry start bits per window
@@ -54,15 +60,18 @@ struct Sym4Lds {
     uint32_t pref[BW];                             // exclusive prefixes of the bitmap words (finish)
     int32_t ebase[NE];                             // B-row start - first product, per non-empty entry
     uint32_t words[BW];                            // first-touch bitmap
-    __device__ int2 *list() { return (int2 *)f1; }
-    __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
-    __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
+    __device__ int32_t *list() { return (int32_t *)f1; }
+    __device__ int32_t *keys() { return (int32_t *)(f1 + LC); }
+    __device__ uint32_t *own() { return (uint32_t *)(f1 + LC + ES); }
 };
 
-// 16 bits of a column's multiplicative hash: f1's bit index; f2's is its top
-// log2(F2B) bits (a coarsening: a column's products share both, which is all
-// the filter's exactness needs).
-__device__ __forceinline__ uint32_t s4_hash16(int32_t c) { return ((uint32_t)c * 0x9E3779B1u) >> 16; }
+// f1's and f2's bit indices: the top bits of two independent multiplicative
+// hashes (f2 a coarsening of f1 made both halves of every false f1 pair
+// possible duplicates: 640 vs 523 listed per 6,900-product row on K3')
+template <int NB>
+__device__ __forceinline__ uint32_t s4_h1(int32_t c) { return ((uint32_t)c * 0x9E3779B1u) >> (32 - ilog2(NB)); }
+template <int NB>
+__device__ __forceinline__ uint32_t s4_h2(int32_t c) { return ((uint32_t)c * 0x85EBCA77u) >> (32 - ilog2(NB)); }
 
 constexpr int SYM4_WPE = 3;   // waves per SIMD the registers must allow (LDS allows 3.5 at U = 4096)
 template <int U, int F1BPP, int KC, int WPB>
@@ -71,7 +80,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
     constexpr int NWIN = LDS::NWIN;
     constexpr int NCH = NWIN / KC;                 // chunks of KC windows
     static_assert(NWIN % KC == 0 && NWIN % 2 == 0, "whole chunks");
-    constexpr int F2SH = 16 - ilog2(LDS::F2B);      // f2 bit = hash16 >> F2SH
     __shared__ LDS lds[WPB];
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)__lane_id();
@@ -193,10 +201,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 for (int t = 0; t < KC; ++t) {
                     const int k = KC * j + t;
                     const bool in = lane < P - 64 * k;
-                    hv[t] = s4_hash16(c[t]);
-                    bit[t] = in ? 1u << (hv[t] & 31) : 0u;
+                    const uint32_t h1 = s4_h1<LDS::F1B>(c[t]);
+                    hv[t] = s4_h2<LDS::F2B>(c[t]);
+                    bit[t] = in ? 1u << (h1 & 31) : 0u;
                     uint32_t o = 0u;   // lanes / windows past the row issue nothing
-                    if (in) o = atomicOr(&L.f1[hv[t] >> 5], bit[t]);
+                    if (in) o = atomicOr(&L.f1[h1 >> 5], bit[t]);
                     old[t] = o;
                 }
 #pragma unroll
@@ -205,8 +214,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                     const bool cand = (old[t] & bit[t]) != 0u;
                     candm |= (cand ? 1ull : 0ull) << k;
                     if (cand) {
-                        const uint32_t h2 = hv[t] >> F2SH;
-                        atomicOr(&L.f2[h2 >> 5], 1u << (h2 & 31));
+                        atomicOr(&L.f2[hv[t] >> 5], 1u << (hv[t] & 31));
                     }
                     if (t & 1) hh2[k >> 1] = (hv[t] << 16) | hv[t - 1];
                 }
@@ -219,14 +227,13 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         // ---- classify: certain first touches -> bitmap words, possible
         // duplicates -> list (product order; their columns gathered after)
         int nl = 0;
-        int2 *list = L.list();
+        int32_t *list = L.list();
 #pragma unroll
         for (int k = 0; k < NWIN; ++k) {
             if (k < nwin) {
                 const int p = 64 * k + lane;
                 const bool in = lane < P - 64 * k;
-                const uint32_t hv = (hh2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                const uint32_t h2 = hv >> F2SH;
+                const uint32_t h2 = (hh2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
                 const uint32_t f2w = L.f2[in ? h2 >> 5 : 0u];
                 const bool poss = in && (((candm >> k) & 1ull) || ((f2w >> (h2 & 31)) & 1u));
                 const uint64_t b = __ballot(in && !poss);
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 const uint64_t pb = __ballot(poss);
                 if (poss) {
                     const int i = nl + (int)__popcll(pb & lt);
-                    if (i < LDS::LC) list[i] = make_int2(0, p);
+                    if (i < LDS::LC) list[i] = p;
                 }
                 nl += (int)__popcll(pb);
             }
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 off[t] = 0u;
                 const int i = t * WAVE + lane;
                 if (i < nl) {
-                    e[t].y = list[i].y;
+                    e[t].y = list[i];
                     off[t] = col_addr(e[t].y >> 6, e[t].y & 63);
                 }
             }

@@ -18,7 +18,7 @@
 // Rows beyond the bounds or whose list overflows go to the retry list (sym2).
 #pragma once
 
-#include "sym3_kernels.hpp"
+#include "sym4_kernels.hpp"
 
 namespace ias {
 namespace dev {
@@ -33,12 +33,15 @@ struct Sym5Lds {
     static constexpr int F2W = F2B / 32;
     static constexpr int BW = U / 32;
     static constexpr int NE = U / 32;              // A entries per row at most
-    static constexpr int LC = U / 8;               // list (8 B per entry) + exact table (8 B per slot) = f1
+    // list (a product index, 4 B per entry) + exact table (8 B per slot) over
+    // f1, whole workgroups: U / 6.4 (U / 8 with 8-byte entries left 17 % / 69 %
+    // of K3''s rows near 8,192 / 16,384 products to sym2)
+    static constexpr int LC = F1W / 3 / T * T;
     static constexpr int ES = LC;
     static constexpr int LT = LC / T;              // list entries per thread
     static constexpr int WPL = BW / T;             // bitmap words per thread in the finish scan
     static constexpr int WIN_PL = NWIN / WAVE;     // windows per lane in wave 0's window scan
-    static_assert(8 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
+    static_assert(4 * LC + 8 * ES <= 4 * F1W, "list and exact table overlay f1");
     static_assert(LC % T == 0 && BW % T == 0 && NWIN % WAVE == 0, "whole workgroups");
     static_assert(F2B <= 65536, "f2 index in 16 bits");
     __attribute__((aligned(16))) uint32_t f1[F1W];
@@ -51,8 +54,8 @@ struct Sym5Lds {
     int32_t nl;                                    // list counter
     int32_t scratch[NW];
     __device__ int32_t *list() { return (int32_t *)f1; }
-    __device__ int32_t *keys() { return (int32_t *)(f1 + 2 * LC); }
-    __device__ uint32_t *own() { return (uint32_t *)(f1 + 2 * LC + ES); }
+    __device__ int32_t *keys() { return (int32_t *)(f1 + LC); }
+    __device__ uint32_t *own() { return (uint32_t *)(f1 + LC + ES); }
 };
 
 template <int U, int NW, int KC>
@@ -63,8 +66,6 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     constexpr int WWIN = LDS::NWIN / NW;           // windows per wave
     constexpr int NCH = WWIN / KC;                 // its chunks of KC windows
     static_assert(WWIN <= WAVE && WWIN % KC == 0 && KC % 2 == 0, "a wave's windows: one candidate mask");
-    constexpr int SH1 = 32 - ilog2(LDS::F1B);      // f1 bit = hash >> SH1
-    constexpr int SH2 = 32 - ilog2(LDS::F2B);      // f2 bit = hash >> SH2 (f1's top bits)
     __shared__ LDS L;
     const int tid = (int)threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
@@ -170,8 +171,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 #pragma unroll
                 for (int t = 0; t < KC; ++t) {
                     const bool in = lane < P - 64 * (k0 + t);
-                    hv[t] = (uint32_t)c[t] * 0x9E3779B1u;
-                    const uint32_t h1 = hv[t] >> SH1;
+                    const uint32_t h1 = s4_h1<LDS::F1B>(c[t]);
+                    hv[t] = s4_h2<LDS::F2B>(c[t]);
                     bit[t] = in ? 1u << (h1 & 31) : 0u;
                     uint32_t o = 0u;   // lanes / windows past the row issue nothing
                     if (in) o = atomicOr(&L.f1[h1 >> 5], bit[t]);
@@ -182,9 +183,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                     const int lk = KC * j + t;
                     const bool cand = (old[t] & bit[t]) != 0u;
                     candm |= (cand ? 1ull : 0ull) << lk;
-                    const uint32_t h2 = hv[t] >> SH2;
-                    if (cand) atomicOr(&L.f2[h2 >> 5], 1u << (h2 & 31));
-                    if (t & 1) hh2[lk >> 1] = (h2 << 16) | (hv[t - 1] >> SH2);
+                    if (cand) atomicOr(&L.f2[hv[t] >> 5], 1u << (hv[t] & 31));
+                    if (t & 1) hh2[lk >> 1] = (hv[t] << 16) | hv[t - 1];
                 }
             }
         }

@@ -12,7 +12,10 @@ CSR_MUL_CSR restatement (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:85-193):
   * ias_dia_mul_dia_into refusing a C that shares memory with an operand, and
     ias_dia_mul_dia_ndiag refusing invalid operands;
   * the block cache of library-allocated device outputs under several host
-    threads allocating and freeing at once.
+    threads allocating and freeing at once;
+  * sym2's retry teams sized from the plan's previous call (rows the sym3 /
+    sym4 / sym5 bins handed back then): a plan whose last call had no retries
+    meets a product whose rows all overflow their lists, and the reverse.
 """
 import ctypes as C
 import threading
@@ -234,3 +237,39 @@ def test_block_cache_concurrent_threads():
     for t in th:
         t.join()
     assert not errors, errors[:4]
+
+
+def retry_rows(crowded, seed=41):
+    """Rows in every sym3 / sym4 / sym5 bin (400 .. 12,000 products, 40
+    columns per B row).  crowded=False: columns drawn from 2^20 (no list
+    overflows); crowded=True: each row's B rows draw from a pool of P/3
+    columns (two thirds of the products repeat a column: every such row
+    overflows its possible-duplicate list and is handed to sym2)."""
+    rng = np.random.default_rng(seed + crowded)
+    per = 40
+    brows, arows = [], []
+    for m in (10, 30, 45, 60, 90, 150, 300):
+        for _ in range(12):
+            base = len(brows)
+            pool = max(per, (m * per) // 3) if crowded else 1 << 20
+            for _ in range(m):
+                brows.append(rng.choice(pool, per, replace=False))
+            arows.append(np.arange(base, len(brows)))
+    return _csr(arows, len(brows), rng), _csr(brows, 1 << 20, rng)
+
+
+def test_retry_grid_follows_plan_history():
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), 0, None), "plan")
+    try:
+        o = ias.opts(output_memory=ias.MEMORY_HOST, device=0, plan=plan)
+        for crowded in (False, True, True, False, True):
+            A, B = retry_rows(crowded)
+            ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+            sa, sb = A.struct(), B.struct()
+            c = ias.Csr()
+            ias.check(ias.lib.ias_csr_mul_csr(C.byref(sa), C.byref(sb), C.byref(c), C.byref(o), None), "mul")
+            got = ias.csr_to_numpy(c)
+            assert_csr_identical(got, ref, f"crowded={crowded}")
+    finally:
+        ias.lib.ias_plan_destroy(plan)
