@@ -68,11 +68,17 @@ struct Sym4Lds {
 // f1's and f2's bit indices: the top bits of two independent multiplicative
 // hashes (f2 a coarsening of f1 made both halves of every false f1 pair
 // possible duplicates: 640 vs 523 listed per 6,900-product row on K3')
+// set bits of m below this lane (v_mbcnt: no 64-bit lane mask held in
+// registers, which the unrolled loops spilled)
+__device__ __forceinline__ int s4_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 template <int NB>
 __device__ __forceinline__ uint32_t s4_h1(int32_t c) { return ((uint32_t)c * 0x9E3779B1u) >> (32 - ilog2(NB)); }
 template <int NB>
 __device__ __forceinline__ uint32_t s4_h2(int32_t c) { return ((uint32_t)c * 0x85EBCA77u) >> (32 - ilog2(NB)); }
 
+constexpr int S4_DEPTH = 2;   // chunk buffers in flight in the filter (sym4, sym5); 3 / 4 within noise
 constexpr int SYM4_WPE = 3;   // waves per SIMD the registers must allow (LDS allows 3.5 at U = 4096)
 template <int U, int F1BPP, int KC, int WPB>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_WPE))) void k_sym4(Sym3Args) {
@@ -84,8 +90,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)__lane_id();
     LDS &L = lds[w];
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint64_t upto = (2ull << lane) - 1ull;   // lane 63: all ones
     const int64_t stride = (int64_t)gridDim.x * WPB;
     int64_t idx = (int64_t)blockIdx.x * WPB + w;
     if (idx >= s3_args()->count) return;
@@ -151,7 +155,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 const int rel = carry + incl - bl;
                 const uint64_t nem = __ballot(bl > 0);
                 if (bl > 0 && rel < P) {
-                    L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
+                    L.ebase[nec + s4_below(nem)] = (int32_t)(bs - rel);
                     atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
                 }
                 carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
@@ -188,14 +192,20 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         uint32_t hh2[NWIN / 2];
         uint64_t candm = 0ull;
         {
-            int32_t ca[KC], cb[KC];
-            gather(0, ca);
+            // a ring of S4_DEPTH chunk buffers: chunks j+1 .. j+S4_DEPTH-1
+            // in flight while chunk j is filtered.  The gathers are
+            // unconditional (chunks past the row read B.col[0]): a gather
+            // under a branch makes the compiler's wait for chunk j assume
+            // the later chunks were not issued, i.e. wait for them too
+            int32_t cbuf[S4_DEPTH][KC];
+#pragma unroll
+            for (int j = 0; j + 1 < S4_DEPTH && j < NCH; ++j) gather(KC * j, cbuf[j]);
 #pragma unroll
             for (int j = 0; j < NCH; ++j) {
-                int32_t(&c)[KC] = (j & 1) ? cb : ca;
-                int32_t(&nx)[KC] = (j & 1) ? ca : cb;
-                if (j + 1 < NCH && KC * (j + 1) < nwin) gather(KC * (j + 1), nx);
-                if (KC * j >= nwin) continue;   // beyond the row: nothing to filter
+                if (KC * j >= nwin) break;   // beyond the row: nothing to filter
+                const int jn = j + S4_DEPTH - 1;
+                if (jn < NCH) gather(KC * jn, cbuf[jn % S4_DEPTH]);
+                const int32_t(&c)[KC] = cbuf[j % S4_DEPTH];
                 uint32_t hv[KC], old[KC], bit[KC];
 #pragma unroll
                 for (int t = 0; t < KC; ++t) {
@@ -220,8 +230,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 }
             }
         }
-        // the next row's details fly during the rest of this one
-        const Det nxt = details(nref);
         tm.mark(1);
         s3_sync();   // f1 dead from here: the list overlays it
         // ---- classify: certain first touches -> bitmap words, possible
@@ -229,27 +237,47 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
         int nl = 0;
         int32_t *list = L.list();
 #pragma unroll
-        for (int k = 0; k < NWIN; ++k) {
-            if (k < nwin) {
-                const int p = 64 * k + lane;
-                const bool in = lane < P - 64 * k;
+        for (int j = 0; j < NCH; ++j) {
+            if (KC * j >= nwin) break;
+            // the chunk's f2 words first (their reads in flight together)
+            uint32_t f2w[KC];
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int k = KC * j + t;
                 const uint32_t h2 = (hh2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                const uint32_t f2w = L.f2[in ? h2 >> 5 : 0u];
-                const bool poss = in && (((candm >> k) & 1ull) || ((f2w >> (h2 & 31)) & 1u));
-                const uint64_t b = __ballot(in && !poss);
-                if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
-                const uint64_t pb = __ballot(poss);
-                if (poss) {
-                    const int i = nl + (int)__popcll(pb & lt);
-                    if (i < LDS::LC) list[i] = p;
+                f2w[t] = L.f2[lane < P - 64 * k ? h2 >> 5 : 0u];
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int k = KC * j + t;
+                if (k < nwin) {
+                    const int p = 64 * k + lane;
+                    const bool in = lane < P - 64 * k;
+                    const uint32_t h2 = (hh2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    // bitwise, not short-circuit: the compiler otherwise sank the
+                    // chunk's f2 reads into a branch per window, each waited on
+                    const uint32_t pv = ((uint32_t)(candm >> k) | (f2w[t] >> (h2 & 31))) & (in ? 1u : 0u);
+                    const bool poss = pv != 0u;
+                    const uint64_t b = __ballot(in && !poss);
+                    if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
+                    const uint64_t pb = __ballot(poss);
+                    if (poss) {
+                        const int i = nl + s4_below(pb);
+                        if (i < LDS::LC) list[i] = p;
+                    }
+                    nl += (int)__popcll(pb);
                 }
-                nl += (int)__popcll(pb);
             }
         }
         s3_sync();
         tm.mark(2);
         const bool retry = 4 * nl > 3 * LDS::LC;
+        // the next row's details fly during the rest of this one, issued
+        // after the listed products' gathers (issued before classify, the
+        // first reuse of a register they load waited for them there)
+        Det nxt;
         if (retry) {
+            nxt = details(nref);
             if (lane == 0) {
                 const int32_t j = atomicAdd(s3_args()->retry_count, 1);
                 s3_args()->retry[j] = ref;
@@ -276,6 +304,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t)
                 if (t * WAVE + lane < nl) e[t].x = *(const int32_t *)(base + off[t]);
+            nxt = details(nref);
             if (nl > 0) {
                 int32_t *keys = L.keys();
                 uint32_t *own = L.own();

@@ -70,20 +70,46 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     const int tid = (int)threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int lane = (int)__lane_id();
-    const uint64_t lt = (1ull << lane) - 1ull;
     for (int i = tid; i < LDS::F1W / 4; i += T) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
     for (int i = tid; i < LDS::F2W; i += T) L.f2[i] = 0u;
 
-    for (int64_t idx = blockIdx.x; idx < s3_args()->count; idx += gridDim.x) {
-        const RowRef ref = s3_args()->list[idx];
+    // a row's details: its list entry, products, and (wave 0) the B-row
+    // extents of its first 64 entries — the next row's are loaded during a
+    // row (without, each row began with three dependent global loads: 3 - 4
+    // us of its ~33)
+    struct Det {
+        RowRef ref;
+        int32_t P, bl;
+        int64_t bs;
+    };
+    auto details = [&](const RowRef &r) {
+        Det d{r, 0, 0, 0};
+        if (r.row >= 0) {
+            d.P = s3_args()->prod[r.row];
+            if (w == 0 && lane < r.n) {
+                d.bl = s3_args()->ax.blen[r.q0 + lane];
+                d.bs = s3_args()->ax.bstart[r.q0 + lane];
+            }
+        }
+        return d;
+    };
+    int64_t idx = blockIdx.x;
+    if (idx >= s3_args()->count) return;
+    Det cur = details(s3_ref(idx));
+    Timer tm;   // timing builds only (phases: 0 staging, 1 filter, 2 classify, 3 exact, 4 finish, 5 clear)
+    tm.start();
+    for (; idx < s3_args()->count; idx += gridDim.x) {
+        const RowRef ref = cur.ref;
         const int32_t row = __builtin_amdgcn_readfirstlane(ref.row);
         const int32_t E = __builtin_amdgcn_readfirstlane(ref.n);
-        const int32_t P = __builtin_amdgcn_readfirstlane(s3_args()->prod[row]);
+        const int32_t P = __builtin_amdgcn_readfirstlane(cur.P);
+        const RowRef nref = s3_ref(idx + gridDim.x);
         if (P > U || E > LDS::NE) {
             if (tid == 0) {
                 const int32_t j = atomicAdd(s3_args()->retry_count, 1);
                 s3_args()->retry[j] = ref;
             }
+            cur = details(nref);
             continue;
         }
         const int nwin = (P + 63) >> 6;
@@ -96,17 +122,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             int carry = 0, nec = 0;
             for (int g = 0; g < E; g += WAVE) {
                 const int e = g + lane;
-                int32_t bl = 0;
-                int64_t bs = 0;
-                if (e < E) {
-                    bl = s3_args()->ax.blen[q0 + e];
-                    bs = s3_args()->ax.bstart[q0 + e];
+                int32_t bl = cur.bl;
+                int64_t bs = cur.bs;
+                if (g > 0) {
+                    bl = 0;
+                    bs = 0;
+                    if (e < E) {
+                        bl = s3_args()->ax.blen[q0 + e];
+                        bs = s3_args()->ax.bstart[q0 + e];
+                    }
                 }
                 const int incl = wave_incl_sum(bl);
                 const int rel = carry + incl - bl;
                 const uint64_t nem = __ballot(bl > 0);
                 if (bl > 0 && rel < P) {
-                    L.ebase[nec + __popcll(nem & lt)] = (int32_t)(bs - rel);
+                    L.ebase[nec + s4_below(nem)] = (int32_t)(bs - rel);
                     atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
                 }
                 carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
@@ -131,6 +161,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
         }
         __syncthreads();
+        tm.mark(0);
         // product p = 64k + l: the byte offset of its B column (beyond P:
         // B.col[0], callers mask it)
         const char *base = (const char *)s3_args()->bcol;
@@ -158,15 +189,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         uint32_t hh2[WWIN / 2];
         uint64_t candm = 0ull;
         {
-            int32_t ca[KC], cb[KC];
-            gather(0, ca);
+            int32_t cbuf[S4_DEPTH][KC];   // sym4's ring (unconditional gathers: see there)
+#pragma unroll
+            for (int j = 0; j + 1 < S4_DEPTH && j < NCH; ++j) gather(j, cbuf[j]);
 #pragma unroll
             for (int j = 0; j < NCH; ++j) {
-                int32_t(&c)[KC] = (j & 1) ? cb : ca;
-                int32_t(&nx)[KC] = (j & 1) ? ca : cb;
                 const int k0 = (wr + j * NW) * KC;
-                if (j + 1 < NCH && k0 + NW * KC < nwin) gather(j + 1, nx);
-                if (k0 >= nwin) continue;   // beyond the row: nothing to filter
+                if (k0 >= nwin) break;   // beyond the row: nothing to filter
+                const int jn = j + S4_DEPTH - 1;
+                if (jn < NCH) gather(jn, cbuf[jn % S4_DEPTH]);
+                const int32_t(&c)[KC] = cbuf[j % S4_DEPTH];
                 uint32_t hv[KC], old[KC], bit[KC];
 #pragma unroll
                 for (int t = 0; t < KC; ++t) {
@@ -189,33 +221,56 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
         }
         __syncthreads();   // f1 dead: the list overlays it
+        tm.mark(1);
         // ---- classify: certain first touches -> bitmap words, possible
         // duplicates -> list (any order; their columns gathered after)
         int32_t *list = L.list();
 #pragma unroll
-        for (int lk = 0; lk < WWIN; ++lk) {
-            const int k = (wr + (lk / KC) * NW) * KC + lk % KC;
-            if (k < nwin) {
-                const int p = 64 * k + lane;
-                const bool in = lane < P - 64 * k;
+        for (int j = 0; j < NCH; ++j) {
+            const int k0 = (wr + j * NW) * KC;
+            if (k0 >= nwin) break;
+            // the chunk's f2 words first (reads in flight together), one list
+            // counter atomic per chunk
+            uint32_t f2w[KC];
+            bool poss[KC];
+            uint64_t pb[KC];
+            int cnt = 0;
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int lk = KC * j + t;
                 const uint32_t h2 = (hh2[lk >> 1] >> (16 * (lk & 1))) & 0xFFFFu;
-                const uint32_t f2w = L.f2[in ? h2 >> 5 : 0u];
-                const bool poss = in && (((candm >> lk) & 1ull) || ((f2w >> (h2 & 31)) & 1u));
-                const uint64_t b = __ballot(in && !poss);
-                if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
-                const uint64_t pb = __ballot(poss);
-                if (pb) {
-                    int at = 0;
-                    if (lane == 0) at = atomicAdd(&L.nl, (int)__popcll(pb));
-                    at = __shfl(at, 0);
-                    const int i = at + (int)__popcll(pb & lt);
-                    if (poss && i < LDS::LC) list[i] = p;
+                f2w[t] = L.f2[lane < P - 64 * (k0 + t) ? h2 >> 5 : 0u];
+            }
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+                const int lk = KC * j + t;
+                const int k = k0 + t;
+                const bool in = lane < P - 64 * k;   // false for windows beyond the row
+                const uint32_t h2 = (hh2[lk >> 1] >> (16 * (lk & 1))) & 0xFFFFu;
+                poss[t] = (((uint32_t)(candm >> lk) | (f2w[t] >> (h2 & 31))) & (in ? 1u : 0u)) != 0u;   // bitwise (sym4)
+                const uint64_t b = __ballot(in && !poss[t]);
+                if (lane == 0 && k < nwin) *(uint64_t *)&L.words[2 * k] = b;
+                pb[t] = __ballot(poss[t]);
+                cnt += (int)__popcll(pb[t]);
+            }
+            if (cnt > 0) {
+                int at = 0;
+                if (lane == 0) at = atomicAdd(&L.nl, cnt);
+                at = __shfl(at, 0);
+#pragma unroll
+                for (int t = 0; t < KC; ++t) {
+                    const int i = at + s4_below(pb[t]);
+                    if (poss[t] && i < LDS::LC) list[i] = 64 * (k0 + t) + lane;
+                    at += (int)__popcll(pb[t]);
                 }
             }
         }
         __syncthreads();
+        tm.mark(2);
         const int32_t nl = L.nl;
+        Det nxt;   // issued after the listed products' gathers (sym4)
         if (4 * nl > 3 * LDS::LC) {
+            nxt = details(nref);
             if (tid == 0) {
                 const int32_t j = atomicAdd(s3_args()->retry_count, 1);
                 s3_args()->retry[j] = ref;
@@ -241,6 +296,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
 #pragma unroll
             for (int t = 0; t < LDS::LT; ++t)
                 if (t * T + tid < nl) e[t].x = *(const int32_t *)(base + off[t]);
+            nxt = details(nref);
             if (nl > 0) {
                 int32_t *keys = L.keys();
                 uint32_t *own = L.own();
@@ -282,6 +338,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                 }
                 __syncthreads();
             }
+            tm.mark(3);
             // ---- finish: nnz and word prefixes (thread-contiguous words)
             const int W = (P + 31) >> 5;
             int cnt = 0;
@@ -330,11 +387,16 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
             }
         }
         // ---- the filters empty for the next row
+        tm.mark(4);
         __syncthreads();
         for (int i = tid; i < LDS::F1W / 4; i += T) ((uint4 *)L.f1)[i] = make_uint4(0u, 0u, 0u, 0u);
         for (int i = tid; i < LDS::F2W; i += T) L.f2[i] = 0u;
         __syncthreads();
+        tm.mark(5);
+        tm.done();
+        cur = nxt;
     }
+    tm.flush(U <= 8192 ? 30 : 31, tid == 0);
 }
 
 }  // namespace dev

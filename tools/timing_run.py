@@ -10,6 +10,8 @@ Phases (spgemm_kernels.hpp, Timer marks):
     3 segment sync, 4 fix-up barrier, 5 duplicate fix-up
   sym-cbm (k_sym_cbm): 0 pass 1, 1 multi bitmap, 2 ranks + minima init,
     3 pass 2, 4 pass 3, 5 word prefixes, 6 placement
+  sym4 / sym5 (k_sym4, k_sym5): 0 staging, 1 filter, 2 classify, 3 exact,
+    4 finish, 5 filter clear
 """
 import argparse
 import ctypes as C
@@ -52,7 +54,7 @@ def main():
         if 24 <= slot <= 26:
             kind, team = "sym3 K=%d" % (8, 12, 16)[slot - 24], 64
         elif slot >= 30:
-            kind, team = ("onepass" if slot == 31 else "op-big"), 512
+            kind, team = ("sym5 U=16384" if slot == 31 else "sym5 U=8192"), 64 * (4 if slot == 31 else 2)
         elif slot == 27:
             kind, team = "sym4", 64
         elif slot == 29:
