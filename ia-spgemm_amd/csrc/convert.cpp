@@ -351,13 +351,14 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
     IAS_TRY(HB.get(B));
     const ias_csr *a = HA.m, *b = HB.m;
     // Estimated device cost per row, in tenths of a product: a fixed cost per
-    // row (binning, per-row passes, launch share) plus its products, those of
-    // rows beyond the LDS bins (hash-partitioned, > 16384 products) weighted
-    // 3.4x.  Calibrated on MI355X (non-negative least squares over K3' and the
-    // eight rank shards of K4 run one at a time, bench.py --as-rank all:
-    // 1.78 ns per row, 10.4 ps per product, +25.2 ps per partitioned-row
-    // product), so the rank holding R-MAT's hub rows gets fewer.
-    constexpr int64_t ROW_COST = 1710, SMALL = 10, BIG = 34, PART_MIN = 16384;
+    // row (binning, per-row passes, launch share) plus its products, weighted
+    // by the symbolic path they take: LDS bins (<= 16,384 products), the
+    // 8-wave sym5 bins (<= 32,768: 2.4x), hash partitions (beyond: 4.4x).
+    // Calibrated on MI355X (non-negative least squares over K3' and the eight
+    // rank shards of K4 run one at a time, bench.py --as-rank all; round 5:
+    // 1.39 ns per row, 7.6 / 18.2 / 33.6 ps per product of the three classes;
+    // DESIGN.md §6), so the rank holding R-MAT's hub rows gets fewer.
+    constexpr int64_t ROW_COST = 1830, SMALL = 10, MID = 24, BIG = 44, MID_MIN = 16384, BIG_MIN = 32768;
     std::vector<int64_t> pref((size_t)a->rows + 1, 0);
     for (int64_t i = 0; i < a->rows; ++i) {
         int64_t prod = 0;
@@ -365,7 +366,7 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
             const int32_t j = a->col[p];
             prod += b->row_ptr[j + 1] - b->row_ptr[j];
         }
-        const int64_t w = ROW_COST + prod * (prod > PART_MIN ? BIG : SMALL);
+        const int64_t w = ROW_COST + prod * (prod > BIG_MIN ? BIG : prod > MID_MIN ? MID : SMALL);
         pref[(size_t)i + 1] = pref[(size_t)i] + w;
     }
     const int64_t total = pref[(size_t)a->rows];

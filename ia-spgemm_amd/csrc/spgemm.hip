@@ -1999,6 +1999,16 @@ static bool sym_feedback() {
     }();
     return on;
 }
+// IAS_SYM_BIG: 0 = rows beyond SYM2_MAX take the hash partitions / column
+// bitmap (A/B), 1 (default) = the sym5<32768> bins when B is too wide for the
+// column bitmap, 2 = also when it is not
+static int big_mode() {
+    static const int m = [] {
+        const char *e = getenv("IAS_SYM_BIG");
+        return e && *e ? atoi(e) : 1;
+    }();
+    return m;
+}
 static bool cbm_enabled() {
     static const bool on = [] {
         const char *e = getenv("IAS_SYM_CBM");
@@ -2032,12 +2042,19 @@ static constexpr BinCfg DW_BINS[] = {{16, 0},   {32, 0},   {64, 1},   {128, 2}, 
 constexpr int32_t SYM2_MAX = 16384;
 constexpr int SYM2_WAVE_CFG_MAX = 3;
 constexpr int SYM2_CFG_WIDE = 8;   // 16 products per lane of a 1024-lane team, one-wave (compact) layout
+// 16,385 .. 32,768 products (round 5), only when B's columns do not fit the
+// column bitmap: k_sym5<32768, 8>, its retries (and all of them when B's
+// entries exceed 32-bit offsets) k_sym_gtab; no sym2 team takes them
+constexpr int SYM_CFG_BIG = 9;
 static constexpr BinCfg SYM2_BINS[] = {{64, 0},    {128, 1},  {256, 2},  {512, 3},  {768, 4},
                                        {1024, 4},  {1536, 5}, {2048, 5}, {3072, 6}, {4096, 6},
                                        {6144, 7},  {8192, 7},
-                                       {12288, SYM2_CFG_WIDE}, {SYM2_MAX, SYM2_CFG_WIDE}
+                                       {12288, SYM2_CFG_WIDE}, {SYM2_MAX, SYM2_CFG_WIDE},
+                                       {24576, SYM_CFG_BIG}, {GT_U, SYM_CFG_BIG}
 };
 constexpr int N_SYM2 = sizeof(SYM2_BINS) / sizeof(SYM2_BINS[0]);
+constexpr int N_SYM2_LDS = N_SYM2 - 2;   // the bins up to SYM2_MAX
+static_assert(SYM2_BINS[N_SYM2_LDS - 1].upper == SYM2_MAX, "bins");
 static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, hipStream_t s);
 constexpr int N_VAL = sizeof(VAL_BINS) / sizeof(VAL_BINS[0]);
 constexpr int N_DW = sizeof(DW_BINS) / sizeof(DW_BINS[0]);
@@ -2065,19 +2082,21 @@ static constexpr bool val_bins_covered() {
 }
 static_assert(val_bins_covered(), "value-bin emission does not cover a bin's table");
 
-// Symbolic LDS bins in use: all of SYM2_BINS, or, when the column-bitmap
-// symbolic applies, those below IAS_SYM_CBM_MIN products (the longer rows
-// join the partitioned bin: k_sym_cbm).
+// Symbolic LDS bins in use: when the column-bitmap symbolic applies, those
+// up to SYM2_MAX (or below IAS_SYM_CBM_MIN products): the longer rows join
+// the partitioned bin (k_sym_cbm); otherwise also the two bins to 32,768
+// products (sym5<32768>; K4: 4.6 vs 31.5 ps per product in the hash
+// partitions), the longer rows hash-partitioned.
 static int sym_nval(bool cbm) {
     static const int nv = [] {
         const char *e = getenv("IAS_SYM_CBM_MIN");
-        if (!e || !*e) return N_SYM2;
+        if (!e || !*e) return N_SYM2_LDS;
         const long v = atol(e);
         int n = 0;
-        while (n < N_SYM2 && SYM2_BINS[n].upper < v) ++n;
+        while (n < N_SYM2_LDS && SYM2_BINS[n].upper < v) ++n;
         return n;
     }();
-    return cbm ? nv : N_SYM2;
+    return cbm ? (big_mode() == 2 ? N_SYM2 : nv) : (big_mode() ? N_SYM2 : N_SYM2_LDS);
 }
 
 static BinSpec sym_spec(int nval = N_SYM2) {
@@ -2207,6 +2226,7 @@ struct StArgs {
 };
 
 static Sym2Layout sym2_layout(int32_t upper, int cfg) {
+    if (cfg == SYM_CFG_BIG) return sym2_layout(SYM2_MAX, SYM2_CFG_WIDE);   // unused: no sym2 team takes these rows
     // 8 filter bits keep the widest bin's team within one CU's LDS
     return Sym2Layout::for_bound((uint32_t)upper, cfg == SYM2_CFG_WIDE     ? Sym2Layout::WIDE
                                                   : cfg <= SYM2_WAVE_CFG_MAX ? Sym2Layout::ONE_WAVE
@@ -2281,8 +2301,18 @@ constexpr int32_t SYM5_MAX = 16384;
 template <int U, int NW>
 static void sym5_launch(const Sym3Args &a, hipStream_t s) {
     auto kern = k_sym5<U, NW, 8>;
-    const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, 0));
-    kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, 0, s>>>(a);
+    static bool done = false;
+    const size_t lds = sizeof(Sym5Lds<U, NW>);
+    allow_lds(kern, done, lds);
+    const int64_t grid = std::min<int64_t>(a.count, resident_blocks(kern, 64 * NW, lds));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), 64 * NW, lds, s>>>(a);
+}
+// k_sym_gtab over a row list (device count a.retry_count), `grid`
+// workgroups each with GT_SLOTS table slots of `keys` / `own`
+constexpr int GT_GRID_MAX = 64;
+static void gtab_launch(const Sym3Args &a, int64_t grid, int32_t *keys, uint32_t *own, hipStream_t s) {
+    grid = std::max<int64_t>(1, std::min<int64_t>(grid, GT_GRID_MAX));
+    k_sym_gtab<<<(unsigned)grid, GT_BLOCK, 0, s>>>(a, keys, own);
 }
 // (its retries: sym2's 1024-lane teams, cfg 7 / SYM2_CFG_WIDE)
 static void sym5_bin(int32_t upper, const Sym3Args &a, hipStream_t s) {
@@ -2605,6 +2635,11 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PSPAN, sizeof(PartSpan) * (size_t)(c1.items + 1)));
     IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
     if (!c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
+    if (ss.nval > N_SYM2_LDS && (c1.count[N_SYM2_LDS + 1] > 0 || c1.count[N_SYM2_LDS + 2] > 0)) {
+        const size_t tab = (size_t)(N_SYM2 - N_SYM2_LDS) * GT_GRID_MAX * GT_SLOTS;
+        IAS_TRY(reserve(B_GTKEY, sizeof(int32_t) * tab));
+        IAS_TRY(reserve(B_GTOWN, sizeof(uint32_t) * tab));
+    }
     const int sym_part = ss.nval + 1;
     // every listed row gets a first-touch bitmap; LDS-bin rows a duplicate list
     IAS_TRY(reserve(B_BITS, sizeof(uint32_t) * (c1.bm_words + 1)));
@@ -2739,6 +2774,27 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         Sym2Args r2 = a2;
         if (retry_feedback() && retry_prev[b & 15] >= 0 && retry_upper[b & 15] == u)
             r2.count = std::min<int32_t>(c, 2 * retry_prev[b & 15] + 2);
+        if (u > SYM5_MAX) {   // SYM_CFG_BIG: sym5<32768>, its retries through the global tables
+            const size_t tab = (size_t)(b - N_SYM2_LDS - 1) * GT_GRID_MAX * GT_SLOTS;
+            int32_t *gk = as<int32_t>(bufs[B_GTKEY]) + tab;
+            uint32_t *go = as<uint32_t>(bufs[B_GTOWN]) + tab;
+            Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
+                        sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
+                        &dc->s3_retry[b & 15]};
+            // IAS_GTAB_ALL=1 (test knob, read per call): the wide-B branch
+            const char *ga = getenv("IAS_GTAB_ALL");
+            if (!c1.wide_b && !(ga && *ga == '1')) {
+                sym5_launch<GT_U, 8>(a5, t);
+                CHECK_LAUNCH("k_sym5", t);
+                gtab_launch(a5, r2.count, gk, go, t);
+            } else {   // B beyond 32-bit offsets: every row of the bin through the global tables
+                a5.retry = SL + st[b];
+                a5.retry_count = &dc->count[b];
+                gtab_launch(a5, c, gk, go, t);
+            }
+            CHECK_LAUNCH("k_sym_gtab", t);
+            return IAS_SUCCESS;
+        }
         if (!c1.wide_b && u > SYM4_MAX && u <= SYM5_MAX) {
             const Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                               sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],

@@ -68,7 +68,9 @@ struct ias_plan {
         // work units of the row-unit numeric pass (num2)
         B_N2CNT, B_N2OFF, B_N2UNIT,
         // sym3's retry lists (rows whose possible-duplicate list overflowed)
-        B_S3RETRY, B_COUNT
+        B_S3RETRY,
+        // k_sym_gtab's global tables (keys, own) for the two bins beyond SYM2_MAX
+        B_GTKEY, B_GTOWN, B_COUNT
     };
     struct Buf {
         void *p = nullptr;

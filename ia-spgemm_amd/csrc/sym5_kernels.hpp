@@ -66,7 +66,8 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
     constexpr int WWIN = LDS::NWIN / NW;           // windows per wave
     constexpr int NCH = WWIN / KC;                 // its chunks of KC windows
     static_assert(WWIN <= WAVE && WWIN % KC == 0 && KC % 2 == 0, "a wave's windows: one candidate mask");
-    __shared__ LDS L;
+    extern __shared__ __attribute__((aligned(16))) unsigned char s5_smem[];   // sizeof(LDS): 90 KB at U = 32,768
+    LDS &L = *reinterpret_cast<LDS *>(s5_smem);
     const int tid = (int)threadIdx.x;
     const int w = __builtin_amdgcn_readfirstlane(tid / WAVE);
     const int lane = (int)__lane_id();
@@ -397,6 +398,142 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
         cur = nxt;
     }
     tm.flush(U <= 8192 ? 30 : 31, tid == 0);
+}
+
+// Rows of 16,385 .. GT_U products when B's columns do not fit the column
+// bitmap (k_sym_cbm) go to k_sym5<GT_U, 8> (same algorithm, 8 waves, 90 KB
+// of LDS); the rows it hands back (list overflow, more than 1,024 entries),
+// and all of those rows when B's entries exceed 32-bit offsets, come here:
+// one 1024-lane workgroup per row, persistent over its list (count read on
+// the device), the exact table in global memory (the workgroup's 2 * GT_U
+// slots of the plan's workspace).  Every product claims its column (CAS,
+// linear probing) and keeps the smallest product index (atomicMin); a
+// product owning its column is its first touch.  Outputs as sym5.  L2
+// atomics: slow, for rare rows.  Table contents changed by atomics are read
+// past the L1 (agent-scope atomic loads), as in k_sym_cbm.
+constexpr int GT_BLOCK = 1024;
+constexpr int GT_U = 32768;          // products per row at most
+constexpr int GT_NE = GT_U / 8;      // A entries per row at most (the bins' 8 x entries <= products)
+constexpr int GT_SLOTS = 2 * GT_U;   // table slots per workgroup
+__global__ __launch_bounds__(GT_BLOCK) void k_sym_gtab(Sym3Args a, int32_t *gkeys, uint32_t *gown) {
+    __shared__ int64_t ebase[GT_NE];         // B-row start - first product, per non-empty entry
+    __shared__ int32_t erel[GT_NE];          // first product of each non-empty entry
+    __shared__ uint32_t words[GT_U / 32];    // first-touch bitmap
+    __shared__ uint32_t pref[GT_U / 32];
+    __shared__ int scratch[GT_BLOCK / WAVE];
+    using TM = Team<GT_BLOCK>;
+    const int tid = (int)threadIdx.x;
+    const int32_t count = *a.retry_count;    // the list's rows (device count)
+    int32_t *keys = gkeys + (size_t)blockIdx.x * GT_SLOTS;
+    uint32_t *own = gown + (size_t)blockIdx.x * GT_SLOTS;
+    auto ld_keys = [](const int32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ld_own = [](const uint32_t *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
+        const RowRef ref = a.retry[idx];
+        const int32_t row = ref.row, E = ref.n;
+        const int32_t P = a.prod[row];
+        if (P > GT_U || E > GT_NE) {   // outside the bins' bounds: never listed here
+            if (tid == 0) a.nnz_row[row] = -1;
+            continue;
+        }
+        // ---- stage the non-empty entries: first product and B-row base
+        int carry = 0, nec = 0;
+        for (int g = 0; g < E; g += GT_BLOCK) {
+            const int e = g + tid;
+            int32_t bl = 0;
+            int64_t bs = 0;
+            if (e < E) {
+                bl = a.ax.blen[ref.q0 + e];
+                bs = a.ax.bstart[ref.q0 + e];
+            }
+            int tot, totn;
+            const int ex = TM::excl_sum(bl, tot, scratch);
+            const int exn = TM::excl_sum(bl > 0 ? 1 : 0, totn, scratch);
+            if (bl > 0) {
+                erel[nec + exn] = carry + ex;
+                ebase[nec + exn] = bs - (carry + ex);
+            }
+            carry += tot;
+            nec += totn;
+        }
+        // ---- the table: a power of two >= 2P slots; the bitmap words
+        int S = 64;
+        while (S < 2 * P) S <<= 1;
+        const uint32_t mask = (uint32_t)S - 1u, sh = 32u - (uint32_t)(31 - __builtin_clz((unsigned)S));
+        for (int i = tid; i < S; i += GT_BLOCK) {
+            (void)atomicExch(&keys[i], EMPTY_KEY);   // performed in L2 before the barrier
+            (void)atomicExch(&own[i], 0xFFFFFFFFu);
+        }
+        const int W = (P + 31) >> 5;
+        for (int i = tid; i < W; i += GT_BLOCK) words[i] = 0u;
+        __syncthreads();
+        // product p's column (entry by binary search over the staged starts)
+        auto column = [&](int32_t p) -> int32_t {
+            int lo = 0, hi = nec - 1;   // the last entry starting at or before p
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (erel[mid] <= p) lo = mid;
+                else hi = mid - 1;
+            }
+            return a.bcol[ebase[lo] + p];
+        };
+        auto slot_of = [&](int32_t c) -> uint32_t {   // the column's slot (it is in the table)
+            uint32_t s = ((uint32_t)c * 0x9E3779B1u) >> sh;
+            while (ld_keys(&keys[s]) != c) s = (s + 1u) & mask;
+            return s;
+        };
+        // ---- claim: every product's column, its smallest product
+        for (int32_t p = tid; p < P; p += GT_BLOCK) {
+            const int32_t c = column(p);
+            uint32_t s = ((uint32_t)c * 0x9E3779B1u) >> sh;
+            for (;;) {
+                const int32_t g = atomicCAS(&keys[s], EMPTY_KEY, c);
+                if (g == EMPTY_KEY || g == c) break;
+                s = (s + 1u) & mask;
+            }
+            atomicMin(&own[s], (uint32_t)p);
+        }
+        __syncthreads();
+        // ---- first touches
+        for (int32_t p = tid; p < P; p += GT_BLOCK) {
+            const uint32_t f = ld_own(&own[slot_of(column(p))]);
+            if (f == (uint32_t)p) atomicOr(&words[p >> 5], 1u << (p & 31));
+        }
+        __syncthreads();
+        // ---- finish: nnz, word prefixes, bitmap, duplicates' first touches
+        int nnz = 0, run = 0;
+        for (int w0 = 0; w0 < W; w0 += GT_BLOCK) {
+            const int wi = w0 + tid;
+            const int cnt = wi < W ? __popc(words[wi]) : 0;
+            int tot;
+            const int ex = TM::excl_sum(cnt, tot, scratch);
+            if (wi < W) pref[wi] = (uint32_t)(run + ex);
+            run += tot;
+        }
+        nnz = run;
+        __syncthreads();
+        const bool heavy = P - nnz > a.dcap;
+        if (!heavy) {
+            const int64_t bmoff = a.bm.off[row];
+            for (int wi = tid; wi < W; wi += GT_BLOCK) {
+                a.bm.bits[bmoff + wi] = words[wi];
+                a.bm.pref[bmoff + wi] = pref[wi];
+            }
+            const int64_t dupoff = a.dup_off[row];
+            for (int32_t p = tid; p < P; p += GT_BLOCK) {
+                const uint32_t f = ld_own(&own[slot_of(column(p))]);
+                if (f != (uint32_t)p) {
+                    const uint32_t rk = pref[p >> 5] + (uint32_t)__popc(words[p >> 5] & ((1u << (p & 31)) - 1u));
+                    a.gdupt[dupoff + ((uint32_t)p - rk)] = (int32_t)f;
+                }
+            }
+        }
+        if (tid == 0) {
+            a.nnz_row[row] = nnz;
+            a.dupn[row] = heavy ? (nnz > a.bm_need ? -3 : -1) : P - nnz;
+        }
+        __syncthreads();   // the table and LDS arrays are the next row's
+    }
 }
 
 }  // namespace dev

@@ -13,6 +13,11 @@ CSR_MUL_CSR restatement (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:85-193):
     ias_dia_mul_dia_ndiag refusing invalid operands;
   * the block cache of library-allocated device outputs under several host
     threads allocating and freeing at once;
+  * rows of 16,385 .. 32,768 products when B is too wide for the column
+    bitmap (k_sym5<32768>, 8 waves, dynamic LDS) and their fall-back through
+    global-memory tables (k_sym_gtab: list overflows, > 1,024 entries, and
+    every row of the bins when forced with IAS_GTAB_ALL=1, the branch taken
+    when B's entries exceed 32-bit offsets);
   * sym2's retry teams sized from the plan's previous call (rows the sym3 /
     sym4 / sym5 bins handed back then): a plan whose last call had no retries
     meets a product whose rows all overflow their lists, and the reverse.
@@ -273,3 +278,47 @@ def test_retry_grid_follows_plan_history():
             assert_csr_identical(got, ref, f"crowded={crowded}")
     finally:
         ias.lib.ias_plan_destroy(plan)
+
+
+def big_rows(seed=53):
+    """B 2^21 columns wide (beyond the column bitmap), A rows of 16,385 ..
+    32,768 products: plain (columns over 2^21), crowded (each row's B rows
+    from a pool of P/3 columns: list overflow), many-entry (1,500 entries of
+    20 products: more entries than sym5 stages), then ordinary rows."""
+    rng = np.random.default_rng(seed)
+    brows, arows = [], []
+    def add(m, per, pool):
+        base = len(brows)
+        for _ in range(m):
+            brows.append(rng.choice(pool, per, replace=False))
+        arows.append(np.arange(base, len(brows)))
+    for m in (420, 500, 640, 780, 830):            # 16.8k .. 33.2k products (the last one beyond: partitions)
+        add(m, 40, 1 << 21)
+    for m in (450, 700):
+        add(m, 40, (m * 40) // 3)
+    add(1500, 20, 1 << 21)
+    nb = len(brows)
+    for _ in range(2000):
+        brows.append(rng.choice(1 << 21, 10, replace=False))
+    for _ in range(800):
+        arows.append(rng.choice(np.arange(nb, len(brows)), 12, replace=False))
+    return _csr(arows, len(brows), rng), _csr(brows, 1 << 21, rng)
+
+
+@pytest.mark.parametrize("force", [0, 1], ids=["sym5-big", "gtab-all"])
+def test_big_rows_wide_b(monkeypatch, force):
+    A, B = big_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    if force:
+        monkeypatch.setenv("IAS_GTAB_ALL", "1")
+    else:
+        monkeypatch.delenv("IAS_GTAB_ALL", raising=False)
+    got, rep = ias.spgemm(A, B)
+    assert rep.max_row_products == 830 * 40
+    assert_csr_identical(got, ref, f"rows beyond 16,384 products, IAS_GTAB_ALL={force}")
+    got_s, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+    for i in range(8):
+        s, e = ref.row_ptr[i], ref.row_ptr[i + 1]
+        o = np.argsort(ref.col[s:e], kind="stable")
+        np.testing.assert_array_equal(got_s.col[s:e], ref.col[s:e][o])
+        np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))
