@@ -110,6 +110,11 @@ __device__ __forceinline__ uint32_t s3_h2(int32_t c, uint32_t n) {
 __device__ __forceinline__ uint32_t s3_h3(int32_t c, uint32_t n) {
     return (uint32_t)(((uint64_t)((uint32_t)c * 0xC2B2AE3Du) * n) >> 32);
 }
+// set bits of m below this lane (v_mbcnt: no 64-bit lane mask held in
+// registers, which the unrolled loops spilled)
+__device__ __forceinline__ int s3_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 __device__ __forceinline__ void s3_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -170,7 +175,6 @@ __device__ __forceinline__ Sym3Row s3_load(const RowRef &ref) {
 template <int K>
 __device__ __forceinline__ void s3_gather(Sym3Lds<K> &L, const Sym3Row &r, int32_t (&c)[K]) {
     const int lane = (int)__lane_id();
-    const uint64_t lt = (1ull << lane) - 1ull;
     const bool fits = r.P <= 64 * K && r.ref.n <= WAVE;
     const int32_t P = fits ? __builtin_amdgcn_readfirstlane(r.P) : 0;
     const int incl = wave_incl_sum(r.bl);
@@ -179,7 +183,7 @@ __device__ __forceinline__ void s3_gather(Sym3Lds<K> &L, const Sym3Row &r, int32
     if (lane < K) L.mask[lane] = 0ull;
     s3_sync();
     if (r.bl > 0 && rel < P) {
-        L.ebase[__popcll(ne & lt)] = (int32_t)(r.bs - rel);
+        L.ebase[s3_below(ne)] = (int32_t)(r.bs - rel);
         atomicOr(&L.mask[(uint32_t)rel >> 6], 1ull << (rel & 63));
     }
     s3_sync();
@@ -220,7 +224,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)__lane_id();
     LDS &L = lds[w];
-    const uint64_t lt = (1ull << lane) - 1ull;
     const int64_t stride = (int64_t)gridDim.x * WPB;
     int64_t idx = (int64_t)blockIdx.x * WPB + w;
     if (idx >= s3_args()->count) return;
@@ -296,10 +299,14 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
         s3_sync();
         tm.mark(2);
         // ---- classify: certain first touches -> bitmap words in the lanes,
-        // possible duplicates -> list (product order) over f1
+        // possible duplicates -> list (product order) over f1 (its reads, the
+        // filter's atomics, are complete: a wave's LDS operations complete in
+        // order)
         uint32_t wd = 0u;   // lane j: bitmap word j
         int32_t nl = 0;
-        uint32_t possm = 0u;
+        int2 *list = L.list();
+        int32_t *keys = L.keys();
+        uint32_t *own = L.own();
         asm volatile("" : "+v"(nwin));
 #pragma unroll
         for (int k0 = 0; k0 < K; k0 += CH) {
@@ -314,29 +321,24 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(sym3_w
                 const int k = k0 + t;
                 const int32_t cc = c[k];
                 const bool in = k < nwin;
-                const bool poss = in && (((candm >> k) & 1u) || ((f2w[t] >> (s3_h2(cc, LDS::F2B) & 31)) & 1u));
-                possm |= (poss ? 1u : 0u) << k;
+                // bitwise, not short-circuit: the compiler otherwise branched
+                // per window around the f2 test
+                const uint32_t pv = ((candm >> k) | (f2w[t] >> (s3_h2(cc, LDS::F2B) & 31))) & (in ? 1u : 0u);
+                const bool poss = pv != 0u;
                 const uint64_t b = __ballot(in && !poss);
                 // words 2k, 2k+1 via LDS into lanes 2k, 2k+1 after the loop (a
                 // select on lane == 2k kept 2K lane masks live in SGPRs: spills)
                 if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
+                const uint64_t pb = __ballot(poss);
+                if (poss) {
+                    const int i = nl + s3_below(pb);
+                    if (i < LDS::LC) list[i] = make_int2(cc, 64 * k + lane);
+                }
+                nl += (int)__popcll(pb);
             }
         }
-        s3_sync();   // every f1 / f2 read done before the list overwrites f1
+        s3_sync();
         wd = lane < 2 * K ? L.words[lane] : 0u;
-        int2 *list = L.list();
-        int32_t *keys = L.keys();
-        uint32_t *own = L.own();
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const bool poss = (possm >> k) & 1u;
-            const uint64_t pb = __ballot(poss);
-            if (poss) {
-                const int i = nl + __popcll(pb & lt);
-                if (i < LDS::LC) list[i] = make_int2(c[k], 64 * k + lane);
-            }
-            nl += __popcll(pb);
-        }
         const int32_t row_nw = (P + 31) >> 5;
         tm.mark(3);
         if constexpr (!DB) {

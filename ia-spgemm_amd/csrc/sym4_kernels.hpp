@@ -68,11 +68,6 @@ struct Sym4Lds {
 // f1's and f2's bit indices: the top bits of two independent multiplicative
 // hashes (f2 a coarsening of f1 made both halves of every false f1 pair
 // possible duplicates: 640 vs 523 listed per 6,900-product row on K3')
-// set bits of m below this lane (v_mbcnt: no 64-bit lane mask held in
-// registers, which the unrolled loops spilled)
-__device__ __forceinline__ int s4_below(uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 template <int NB>
 __device__ __forceinline__ uint32_t s4_h1(int32_t c) { return ((uint32_t)c * 0x9E3779B1u) >> (32 - ilog2(NB)); }
 template <int NB>
@@ -155,7 +150,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                 const int rel = carry + incl - bl;
                 const uint64_t nem = __ballot(bl > 0);
                 if (bl > 0 && rel < P) {
-                    L.ebase[nec + s4_below(nem)] = (int32_t)(bs - rel);
+                    L.ebase[nec + s3_below(nem)] = (int32_t)(bs - rel);
                     atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
                 }
                 carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
@@ -262,7 +257,7 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(SYM4_W
                     if (lane == 0) *(uint64_t *)&L.words[2 * k] = b;
                     const uint64_t pb = __ballot(poss);
                     if (poss) {
-                        const int i = nl + s4_below(pb);
+                        const int i = nl + s3_below(pb);
                         if (i < LDS::LC) list[i] = p;
                     }
                     nl += (int)__popcll(pb);

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                 const int rel = carry + incl - bl;
                 const uint64_t nem = __ballot(bl > 0);
                 if (bl > 0 && rel < P) {
-                    L.ebase[nec + s4_below(nem)] = (int32_t)(bs - rel);
+                    L.ebase[nec + s3_below(nem)] = (int32_t)(bs - rel);
                     atomicOr(&L.smask[(uint32_t)rel >> 6], 1ull << (rel & 63));
                 }
                 carry += __builtin_amdgcn_readlane(incl, WAVE - 1);
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(3))) vo
                 at = __shfl(at, 0);
 #pragma unroll
                 for (int t = 0; t < KC; ++t) {
-                    const int i = at + s4_below(pb[t]);
+                    const int i = at + s3_below(pb[t]);
                     if (poss[t] && i < LDS::LC) list[i] = 64 * (k0 + t) + lane;
                     at += (int)__popcll(pb[t]);
                 }
