@@ -1452,8 +1452,10 @@ __device__ __forceinline__ void bitonic_keys(int32_t *sk, uint32_t cap) {
         }
     }
 }
-// a bucket of more keys than this sends the row to bitonic_keys (8x the mean of 4)
-constexpr uint32_t SORTB_HEAVY = 32;
+// a bucket of more keys than this sends the row to bitonic_keys: its m^2 / TEAM
+// rank loop then costs about what the bitonic sort does (32 = 8x the mean of
+// 4 sent most of K3's R-MAT rows there: sorted K3' 19.5 -> 41.7 ms)
+constexpr uint32_t SORTB_HEAVY = 256;
 
 __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t *len, int64_t stride,
                                               int64_t row, int64_t &o, int32_t &n) {
@@ -1982,6 +1984,17 @@ static bool retry_print() {
     static const bool on = [] {
         const char *e = getenv("IAS_RETRY_PRINT");
         return e && *e == '1';
+    }();
+    return on;
+}
+// k_fixup_big (lists > 4,096 duplicates) at the head of the fix-up stream,
+// once its rows' units are done, instead of between the streaming pass's
+// launches on the pass's stream: K3' numeric 5.16 -> 5.06 ms, K3 +0.15 ms
+// (round 5, profiles/r05/ab/fixbig_*); IAS_FIXBIG_SIDE=0: the pass's stream
+static bool fixbig_side() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_FIXBIG_SIDE");
+        return !(e && *e == '0');
     }();
     return on;
 }
@@ -3049,7 +3062,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                         n2_mask |= 1 << k;
                     }
                     if (fix_split && k < 2) HIPC(hipEventRecord(fix_ev[k], t));
-                    if (fix_split && k == 0) IAS_TRY(launch_fix(t, 0));
+                    if (fix_split && k == 0 && !fixbig_side()) IAS_TRY(launch_fix(t, 0));
                 }
                 fix_lane = lane_no;   // the fix-ups: the stream after this one
             }
@@ -3078,6 +3091,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     if (fix_split) {
         hipStream_t f = (hipStream_t)side_stream(fix_lane);
         HIPC(hipStreamWaitEvent(f, fix_ev[0], 0));
+        if (fixbig_side()) IAS_TRY(launch_fix(f, 0));
         IAS_TRY(launch_fix(f, 1));
         HIPC(hipStreamWaitEvent(f, fix_ev[1], 0));
         IAS_TRY(launch_fix(f, 2));

@@ -141,9 +141,10 @@ def test_cbm_diag_off_without_knob(cbm_case, monkeypatch):
 def skewed_rows(seed=23):
     """C rows whose columns cluster with far outliers, for every bucket-sort
     team size (rows of ~100 .. ~8,000 entries): A row i takes m_i B rows whose
-    columns lie in [0, 20000) except one column near 2^20 - 1."""
+    columns lie in [0, 4000) except one column near 2^20 - 1 (the long rows put
+    hundreds of keys in each of a few buckets)."""
     rng = np.random.default_rng(seed)
-    brows = [np.concatenate([rng.choice(20000, 15, replace=False), [(1 << 20) - 1 - i]]) for i in range(3000)]
+    brows = [np.concatenate([rng.choice(4000, 15, replace=False), [(1 << 20) - 1 - i]]) for i in range(3000)]
     arows = [rng.choice(3000, m, replace=False) for m in (8, 30, 60, 120, 250, 500, 1000, 2000)]
     arows += [rng.choice(3000, 10, replace=False) for _ in range(200)]
     return _csr(arows, 3000, rng), _csr(brows, 1 << 20, rng)
