@@ -5,7 +5,7 @@
 #   SERIAL_LIB=name  IAS_SERIAL=1 rocprofv3 kernel stats of that variant
 #   TRACE_LIB=name   concurrent rocprofv3 kernel trace (timeline) of that variant
 #   HIPTRACE=1       HIP API trace of the driver's bench command (one-shot leg)
-# A name may be lib+VAR=value: that library with one environment variable set.
+# A name may be lib+VAR=value[+VAR2=value2...]: that library with those environment variables.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,7 +16,7 @@ for rep in $(seq 1 ${REPS:-2}); do
   for name in $NAMES; do
     # name = lib or lib+VAR=value (an environment variant of a library)
     lib=${name%%+*}; envv=; [ "$lib" != "$name" ] && envv=${name#*+}
-    env $envv IAS_LIB=$PWD/build_var/libias_$lib.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline \
+    env ${envv//+/ } IAS_LIB=$PWD/build_var/libias_$lib.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline \
        --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/ab_${name}_$rep.json 2> $OUT/ab_${name}_$rep.err || exit $?
     echo "$name $rep $(python3 -c "import json;d=json.load(open('$OUT/ab_${name}_$rep.json'));print(d['value'],d['ms_per_step'],d['phases_ms_rank0'],d['roofline'].get('ms_per_launch'))")" >> $S
   done
