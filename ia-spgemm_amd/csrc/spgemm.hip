@@ -1991,6 +1991,13 @@ static bool retry_print() {
 // once its rows' units are done, instead of between the streaming pass's
 // launches on the pass's stream: K3' numeric 5.16 -> 5.06 ms, K3 +0.15 ms
 // (round 5, profiles/r05/ab/fixbig_*); IAS_FIXBIG_SIDE=0: the pass's stream
+static bool part_side() {
+    static const bool on = [] {
+        const char *e = getenv("IAS_PART_SIDE");
+        return e && *e == '1';
+    }();
+    return on;
+}
 static bool fixbig_side() {
     static const bool on = [] {
         const char *e = getenv("IAS_FIXBIG_SIDE");
@@ -2697,9 +2704,15 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         double load[NSIDE] = {};
         std::vector<std::pair<double, int>> jobs;
         auto weight = [&](int b, double serial_w) { return fb && sym_w[b] > 0.0 ? sym_w[b] : serial_w; };
+        // the partitioned rows (one workgroup per row or partition, grids far
+        // beyond residency) run on the plan stream: on a side stream their
+        // dispatch held its hardware queue, and the bins of the stream sharing
+        // that queue waited behind it (K3: 3.2 ms of one queue idle at the
+        // end of the symbolic phase); IAS_PART_SIDE=1: a side stream (A/B)
         if (c1.count[sym_part] > 0) {
             sym_est[sym_part] = (double)c1.part_prod;
-            jobs.push_back({weight(sym_part, cbm ? CBM_COST : 40.0) * sym_est[sym_part], sym_part});
+            if (part_side())
+                jobs.push_back({weight(sym_part, cbm ? CBM_COST : 40.0) * sym_est[sym_part], sym_part});
         }
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
@@ -2721,7 +2734,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         bin_rec[b] = true;
     };
     if ((c = c1.count[sym_part]) > 0) {
-        hipStream_t t = (hipStream_t)side_stream(sym_lane[sym_part]);
+        hipStream_t t = part_side() ? (hipStream_t)side_stream(sym_lane[sym_part]) : s;
         bin_mark(sym_part, t, 0);
         if (cbm) {
             static bool cbm_done = false;
@@ -2962,12 +2975,17 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     // the streaming pass — the phase's critical path — is launched first: the
     // host issues ~30 API calls for the others (~60 us on K3')
     IAS_TRY(fork());
-    int lane_no = (num_count[part_bin] > 0 ? 1 : 0) + (num_count[wide_bin] > 0 ? 1 : 0);
+    int lane_no = (num_count[part_bin] > 0 && part_side() ? 1 : 0) + (num_count[wide_bin] > 0 ? 1 : 0);
     for (int i = 0; i < N_DW; ++i) lane_no += num_count[ns.nval + 3 + i] > 0 ? 1 : 0;
     auto launch_tables = [&]() -> ias_status {
         int tl = 0;
+        // the partition tables (one workgroup per (row, partition), grids far
+        // beyond residency) on the plan stream: on a side stream their
+        // dispatch held the hardware queue, and the fix-ups and short rows of
+        // the stream sharing it waited behind (K3: 3.9 ms of fix-ups after
+        // the last streaming launch); IAS_PART_SIDE=1: a side stream (A/B)
         if (num_count[part_bin] > 0) {
-            hipStream_t t = (hipStream_t)side_stream(tl++);
+            hipStream_t t = part_side() ? (hipStream_t)side_stream(tl++) : s;
             k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, t>>>(
                 ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
             CHECK_LAUNCH("k_numeric_part", t);
