@@ -41,6 +41,9 @@ def test_only_c_symbols_exported():
 
 def test_version_and_status_strings():
     assert ias.lib.ias_abi_version() == 6
+    # the header the library was built from says the same (build() checks it)
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "ias.h")).read()
+    assert int(re.search(r"#define IAS_ABI_VERSION (\d+)", hdr).group(1)) == ias.lib.ias_abi_version()
     for s in range(12):
         assert ias.lib.ias_status_string(s)
     assert ias.lib.ias_status_string(99) == b"unknown status"
