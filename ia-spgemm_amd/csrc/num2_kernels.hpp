@@ -23,6 +23,8 @@
 // flat pass's reverse-order 4- and 8-byte scatter stores took ~3 of its 5 ms.
 #pragma once
 
+#include <type_traits>
+
 #include "spgemm_kernels.hpp"
 #include "spgemm_engine.hpp"   // Counters
 
@@ -99,18 +101,30 @@ __device__ __forceinline__ void st16(void *p, uint4 v) {
 constexpr int N2_K = 4;
 
 constexpr int N2_WPE = 1;   // minimum waves per SIMD the register allocation must allow (1: no cap)
+// W64: B's entries beyond 2^29 (byte offsets of its values beyond 32 bits):
+// 64-bit gather addresses.  Otherwise (round 5) every gather is a 32-bit
+// byte offset from the array's SGPR base, the entries' bases are 32-bit, and
+// C's positions within a step are 32-bit offsets from a uniform base: the
+// 64-bit address arithmetic was ~a fifth of the kernel's VALU instructions.
+// ORD: C's order (0: reverse first touch, 1: forward), a template argument
+// so the staging index needs no select.
+template <bool W64, int ORD>
 __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_WPE))) void k_num2(Num2Args a,
                                                                                                  Out out) {
     constexpr int K = N2_K;
     constexpr int PASS = 64 * K;   // staged C entries per step (at most one per product)
+    using BsT = typename std::conditional<W64, int64_t, int32_t>::type;
     struct Ent {
-        int64_t bs;   // B-row start - row-relative first product of the entry
+        BsT bs;       // B-row start - row-relative first product of the entry
         double av;
     };
     __shared__ Ent ent[N2_WPB][N2_ENT];
     __shared__ unsigned long long wmask[N2_WPB][K];
-    __shared__ __attribute__((aligned(16))) int32_t scol[N2_WPB][PASS];
-    __shared__ __attribute__((aligned(16))) double sval[N2_WPB][PASS];
+    // staged in C's order, aligned as C is: slot = C position - a base
+    // congruent to C's 16-byte pieces, so each piece is one 16-byte LDS read
+    __shared__ __attribute__((aligned(16))) int32_t scol[N2_WPB][PASS + 4];   // rows of 1,040 B
+    __shared__ __attribute__((aligned(16))) double sval[N2_WPB][PASS + 2];    // rows of 2,064 B
+    static_assert((PASS + 4) * 4 % 16 == 0 && (PASS + 2) * 8 % 16 == 0, "16-byte aligned staging rows");
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)(threadIdx.x & (WAVE - 1));
     const int64_t u = (int64_t)blockIdx.x * N2_WPB + w;
@@ -144,13 +158,13 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     if (pb <= pa) return;
     // non-empty entries, compacted in order
     const uint64_t ne = __ballot(bl > 0);
-    if (bl > 0) ent[w][__popcll(ne & ((1ull << lane) - 1ull))] = Ent{bs - rel, av};
+    if (bl > 0) ent[w][__popcll(ne & ((1ull << lane) - 1ull))] = Ent{(BsT)(bs - rel), av};
     const int64_t cst = out.start(row);
     const int32_t nnz = out.len[row];
     const int64_t bmo = a.bm.off[row];
     const int64_t dbase = a.dup_off[row];
-    const int64_t cbase = out.order == 0 ? cst + nnz - 1 : cst;   // C position of rank 0
-    const uint64_t upto = (2ull << lane) - 1ull;                // bits 0..lane
+    const int64_t cbase = ORD == 0 ? cst + nnz - 1 : cst;   // C position of rank 0
+    const uint64_t upto = (2ull << lane) - 1ull;           // bits 0..lane
     const uint32_t below = (1u << (lane & 31)) - 1u;
     // 16-byte pieces start where the destination address is 16-byte aligned
     const int64_t cph = (int64_t)(((uintptr_t)out.col >> 2) & 3u);
@@ -172,6 +186,8 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
         // loads read one of two addresses
         uint32_t wp;
     };
+    const char *bcol = (const char *)a.bcol;
+    const char *bval = (const char *)a.bval;
     // gathers of the step at window pw0.  Branch-free (clamped addresses for
     // the lanes and words outside the unit), so that the wait for a step's
     // loads counts exactly the loads issued after them.
@@ -189,9 +205,15 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
             const int ecur = (int)__popcll(__ballot(bl > 0 && rel < pw));
             const int ei = ecur + (int)__popcll(wmask[w][k] & upto) - 1;
             S.e[k] = ei > 0 ? ei : 0;
-            const int64_t kb = (p >= pa && p < pb) ? ent[w][S.e[k]].bs + p : 0;
-            S.c[k] = a.bcol[kb];
-            S.bv[k] = a.bval[kb];
+            if constexpr (W64) {
+                const int64_t kb = (p >= pa && p < pb) ? ent[w][S.e[k]].bs + p : 0;
+                S.c[k] = a.bcol[kb];
+                S.bv[k] = a.bval[kb];
+            } else {
+                const uint32_t kb = (p >= pa && p < pb) ? (uint32_t)(ent[w][S.e[k]].bs + p) : 0u;
+                S.c[k] = *(const int32_t *)(bcol + (kb << 2));
+                S.bv[k] = *(const double *)(bval + (kb << 3));
+            }
         }
         {
             const int j = lane & (2 * K - 1);
@@ -212,6 +234,14 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     };
     // stage the step's first touches by rank, park its duplicates, flush
     auto store = [&](int32_t pw0, const Step &S) {
+        // the step's C positions: ranks r0 .. r0 + nft - 1; ORD 0 puts rank r
+        // at cbase - r (xhi = cbase - r0 + 1 known before the step), ORD 1 at
+        // cbase + r (xlo = cbase + r0).  Staging bases: the step's lowest
+        // possible position rounded down to a 16-byte piece of C.
+        const int64_t lo = ORD == 0 ? cbase - r0 + 1 - PASS : cbase + r0;
+        const int64_t xbc = ((lo + cph) & ~3ll) - cph, xbv = ((lo + vph) & ~1ll) - vph;
+        // slot of rank rk: ORD 0: (cbase - xb) - rk, ORD 1: (cbase - xb) + rk
+        const int32_t oc = (int32_t)(cbase - xbc), ov = (int32_t)(cbase - xbv);
         int nft = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -223,53 +253,52 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
             const int32_t rk = (int32_t)(pre + (uint32_t)__popc(word & below));
             const double prod = ent[w][S.e[k]].av * S.bv[k];
             if (ft) {
-                scol[w][rk - r0] = S.c[k];
-                sval[w][rk - r0] = out.first_assign ? prod : 0.0 + prod;
+                scol[w][ORD == 0 ? oc - rk : oc + rk] = S.c[k];
+                sval[w][ORD == 0 ? ov - rk : ov + rk] = out.first_assign ? prod : 0.0 + prod;
             } else if (in) {
                 a.dupval[dbase + (p - rk)] = prod;
             }
             nft += __popcll(__ballot(ft));
         }
         wave_sync();
-        // C positions of the staged ranks r0 .. r0 + nft - 1: [xlo, xhi)
-        const int64_t xlo = out.order == 0 ? cbase - (r0 + nft - 1) : cbase + r0;
+        // C positions of the staged ranks: [xlo, xhi)
+        const int64_t xlo = ORD == 0 ? cbase - (r0 + nft - 1) : cbase + r0;
         const int64_t xhi = xlo + nft;
-        const int64_t i0 = out.order == 0 ? cbase - r0 : -(cbase + r0);
-        auto idx = [&](int64_t x) -> int32_t { return out.order == 0 ? (int32_t)(i0 - x) : (int32_t)(x + i0); };
         // whole 16-byte pieces: [a4, e4) of the columns, [a2, e2) of the values
         const int64_t a4 = ((xlo + cph + 3) & ~3ll) - cph, e4 = ((xhi + cph) & ~3ll) - cph;
         const int64_t a2 = ((xlo + vph + 1) & ~1ll) - vph, e2 = ((xhi + vph) & ~1ll) - vph;
+        {
+            const int32_t sb = (int32_t)(a4 - xbc), span = (int32_t)(e4 - a4);
+            int32_t *cb = out.col + a4;   // uniform base, 32-bit lane offsets
 #pragma unroll
-        for (int it = 0; it < (PASS / 4 + WAVE) / WAVE; ++it) {
-            const int64_t x = a4 + 4ll * (lane + WAVE * it);
-            if (x + 4 <= e4) {
-                uint4 v;
-                v.x = (uint32_t)scol[w][idx(x)];
-                v.y = (uint32_t)scol[w][idx(x + 1)];
-                v.z = (uint32_t)scol[w][idx(x + 2)];
-                v.w = (uint32_t)scol[w][idx(x + 3)];
-                st16(&out.col[x], v);
+            for (int it = 0; it < (PASS / 4 + WAVE) / WAVE; ++it) {
+                const int32_t d = 4 * (lane + WAVE * it);
+                if (d + 4 <= span) st16(cb + d, ((const uint4 *)scol[w])[(sb + d) >> 2]);   // sb + d: a multiple of 4
             }
         }
+        {
+            const int32_t sb = (int32_t)(a2 - xbv), span = (int32_t)(e2 - a2);
+            double *vb = out.val + a2;
 #pragma unroll
-        for (int it = 0; it < (PASS / 2 + WAVE) / WAVE; ++it) {
-            const int64_t x = a2 + 2ll * (lane + WAVE * it);
-            if (x + 2 <= e2) {
-                const double d0 = sval[w][idx(x)], d1 = sval[w][idx(x + 1)];
-                uint4 v;
-                __builtin_memcpy(&v.x, &d0, 8);
-                __builtin_memcpy(&v.z, &d1, 8);
-                st16(&out.val[x], v);
+            for (int it = 0; it < (PASS / 2 + WAVE) / WAVE; ++it) {
+                const int32_t d = 2 * (lane + WAVE * it);
+                if (d + 2 <= span) st16(vb + d, ((const uint4 *)sval[w])[(sb + d) >> 1]);   // sb + d: even
             }
         }
         // the partial pieces at both ends: lanes 0-2 / 3-5 columns, 6 / 7 values
-        int64_t xc = -1, xv = -1;
-        if (lane < 3) xc = xlo + lane < min(a4, xhi) ? xlo + lane : -1;
-        else if (lane < 6) xc = max(e4, a4) + (lane - 3) < xhi ? max(e4, a4) + (lane - 3) : -1;
-        else if (lane == 6) xv = xlo < min(a2, xhi) ? xlo : -1;
-        else if (lane == 7) xv = max(e2, a2) < xhi ? max(e2, a2) : -1;
-        if (xc >= 0) __builtin_nontemporal_store(scol[w][idx(xc)], &out.col[xc]);
-        if (xv >= 0) __builtin_nontemporal_store(sval[w][idx(xv)], &out.val[xv]);
+        {
+            int32_t dc = -1, dv = -1;   // offsets from xlo
+            const int32_t ha4 = (int32_t)(min(a4, xhi) - xlo), he4 = (int32_t)(max(e4, a4) - xlo);
+            const int32_t ha2 = (int32_t)(min(a2, xhi) - xlo), he2 = (int32_t)(max(e2, a2) - xlo);
+            const int32_t n32 = nft;
+            if (lane < 3) dc = lane < ha4 ? lane : -1;
+            else if (lane < 6) dc = he4 + (lane - 3) < n32 ? he4 + (lane - 3) : -1;
+            else if (lane == 6) dv = 0 < ha2 ? 0 : -1;
+            else if (lane == 7) dv = he2 < n32 ? he2 : -1;
+            const int32_t sc0 = (int32_t)(xlo - xbc), sv0 = (int32_t)(xlo - xbv);
+            if (dc >= 0) __builtin_nontemporal_store(scol[w][sc0 + dc], out.col + xlo + dc);
+            if (dv >= 0) __builtin_nontemporal_store(sval[w][sv0 + dv], out.val + xlo + dv);
+        }
         r0 += nft;
         wave_sync();
     };

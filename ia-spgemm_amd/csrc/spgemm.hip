@@ -194,10 +194,14 @@ __global__ __launch_bounds__(AN_BLOCK) void k_an_entries(Rows A, Rows B, int64_t
         sum += bn[u];
     }
     if (ax.wide_b) {
-        bool wide = false;
+        bool wide = false, widev = false;
 #pragma unroll
-        for (int u = 0; u < AN_U; ++u) wide |= bs[u] + bn[u] > (1ll << 30);
+        for (int u = 0; u < AN_U; ++u) {
+            wide |= bs[u] + bn[u] > (1ll << 30);
+            widev |= bs[u] + bn[u] > (1ll << 29);
+        }
         if (wide) *ax.wide_b = 1;
+        if (widev && ax.wide_v) *ax.wide_v = 1;
     }
 #pragma unroll
     for (int u = 0; u < AN_U; ++u) {
@@ -2585,7 +2589,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     int64_t *poff = as<int64_t>(bufs[B_POFF]);
     if (a_entries > 0)   // one block per scan tile (its B-row length sum -> B_PART2)
         k_an_entries<<<(unsigned)nbe, AN_BLOCK, 0, s>>>(A, B, a_entries,
-                                                        AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, &dc->wide_b},
+                                                        AxOut{as<int64_t>(bufs[B_AXS]), axl, nullptr, &dc->wide_b, &dc->wide_v},
                                                         as<int64_t>(bufs[B_PART2]));
     CHECK_LAUNCH("expanded A", s);
     if (a_entries > 0) {
@@ -2636,6 +2640,11 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         return IAS_ERROR_INVALID_ARGUMENT;
     }
     flops = (int64_t)c1.flops;
+    wide_v = c1.wide_v != 0;
+    if (!wide_v) {   // IAS_WIDE_V=1: test knob, the 64-bit-address streaming pass on any input
+        const char *e = getenv("IAS_WIDE_V");
+        wide_v = e && *e == '1';
+    }
     small = flops < SMALL_FLOPS;
     max_prod = c1.max_prod;
 
@@ -3074,7 +3083,14 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                         nk.units += cut[k];
                         nk.nunits = nu;
                         if (rep) HIPC(hipEventRecord(n2_ev[2 * k], t));
-                        k_num2<<<(unsigned)((nu + N2_WPB - 1) / N2_WPB), 64 * N2_WPB, 0, t>>>(nk, out);
+                        const unsigned g = (unsigned)((nu + N2_WPB - 1) / N2_WPB);
+                        if (wide_v) {
+                            if (out.order == 0) k_num2<true, 0><<<g, 64 * N2_WPB, 0, t>>>(nk, out);
+                            else k_num2<true, 1><<<g, 64 * N2_WPB, 0, t>>>(nk, out);
+                        } else {
+                            if (out.order == 0) k_num2<false, 0><<<g, 64 * N2_WPB, 0, t>>>(nk, out);
+                            else k_num2<false, 1><<<g, 64 * N2_WPB, 0, t>>>(nk, out);
+                        }
                         if (rep) HIPC(hipEventRecord(n2_ev[2 * k + 1], t));
                         ++n2_launches;
                         n2_mask |= 1 << k;

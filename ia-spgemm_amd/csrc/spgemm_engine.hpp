@@ -52,6 +52,7 @@ struct Counters {
     int32_t cbm_hits;             // k_sym_cbm branches taken (IAS_CBM_FORCE set: ias_last_diag)
     int32_t s3_retry[16];         // sym3 / sym4: rows handed to sym2, per bin (bin & 15; retry lists)
     int32_t wide_b;               // a selected B row ends beyond 2^30 entries: no sym3 (32-bit offsets)
+    int32_t wide_v;               // one ends beyond 2^29: k_num2 with 64-bit gather addresses
     int32_t count[MAX_BINS];      // rows per bin (counting pass)
     int32_t cursor[MAX_BINS];     // scatter-pass cursors
 };
@@ -103,6 +104,7 @@ struct ias_plan {
     int64_t n_rows = 0;
     int64_t n_cols = 0;      // C's columns
     bool cbm_path = false;   // partitioned rows: one LDS column bitmap per row (k_sym_cbm)
+    bool wide_v = false;     // B entries beyond 2^29 among the selected rows (k_num2<true, …>)
     int64_t n_entries = 0;   // stored entries of A (expanded-A length)
     int64_t nnz_total = 0;
     int64_t flops = 0;

@@ -113,6 +113,7 @@ struct AxOut {
     int32_t *blen;
     double *aval;
     int32_t *wide_b;   // nullable: set to 1 when a selected B row ends beyond 2^30 entries
+    int32_t *wide_v;   // nullable: set to 1 when one ends beyond 2^29 (k_num2's 32-bit value offsets)
 };
 
 // A row of a bin list: its first expanded-A entry and entry count.

@@ -20,7 +20,11 @@ CSR_MUL_CSR restatement (IA-SPGEMM-CPU_release/detail/csr/common_csr.h:85-193):
     when B's entries exceed 32-bit offsets);
   * sym2's retry teams sized from the plan's previous call (rows the sym3 /
     sym4 / sym5 bins handed back then): a plan whose last call had no retries
-    meets a product whose rows all overflow their lists, and the reverse.
+    meets a product whose rows all overflow their lists, and the reverse;
+  * B rows selected beyond 2^29 and 2^30 entries (a padded B): the streaming
+    numeric pass with 64-bit gather addresses, and the symbolic bins that
+    take over from the 32-bit-offset ones; the 64-bit pass forced on an
+    ordinary input (IAS_WIDE_V=1).
 """
 import ctypes as C
 import threading
@@ -323,3 +327,52 @@ def test_big_rows_wide_b(monkeypatch, force):
         o = np.argsort(ref.col[s:e], kind="stable")
         np.testing.assert_array_equal(got_s.col[s:e], ref.col[s:e][o])
         np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))
+
+
+def _padded_b(B, pad):
+    """B behind a first row of `pad` entries (column 0, value 0) that A never
+    selects: every selected row's entries sit beyond `pad`."""
+    rp = np.concatenate([[0], B.row_ptr + pad]).astype(np.int64)
+    col = np.zeros(pad + B.col.size, np.int32)   # untouched pages stay unallocated
+    col[pad:] = B.col
+    val = np.zeros(pad + B.val.size, np.float64)
+    val[pad:] = B.val
+    return ias.HostCsr(B.rows + 1, B.cols, rp, col, val)
+
+
+def _check_sorted(got_s, ref, rows):
+    for i in rows:
+        s, e = ref.row_ptr[i], ref.row_ptr[i + 1]
+        o = np.argsort(ref.col[s:e], kind="stable")
+        np.testing.assert_array_equal(got_s.col[s:e], ref.col[s:e][o])
+        np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))
+
+
+@pytest.mark.parametrize("pad", [(1 << 29) + 1000, (1 << 30) + 1000], ids=["beyond-2^29", "beyond-2^30"])
+def test_b_entries_beyond_32bit_offsets(pad):
+    """B's selected rows start beyond 2^29 entries (the streaming numeric pass
+    gathers through 64-bit addresses: k_num2<true, …>) and beyond 2^30 (no
+    sym3 / sym4 / sym5: sym2 and the global tables)."""
+    R = ias.gen_rmat(13, 16, seed=71)
+    ref = ob.csr_mul_csr(ob.Mat.of(R), ob.Mat.of(R))
+    A = ias.HostCsr(R.rows, R.cols + 1, R.row_ptr, R.col + 1, R.val)
+    B = _padded_b(R, pad)
+    got, _ = ias.spgemm(A, B)
+    assert_csr_identical(got, ref, f"B entries from {pad}")
+    got_s, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+    _check_sorted(got_s, ref, range(0, R.rows, 97))
+
+
+@pytest.mark.parametrize("order", [0, 1], ids=["reference", "sorted"])
+def test_wide_v_knob(monkeypatch, order):
+    """IAS_WIDE_V=1: the 64-bit-address streaming pass on an ordinary input."""
+    R = ias.gen_rmat(14, 16, seed=73)
+    ref = ob.csr_mul_csr(ob.Mat.of(R), ob.Mat.of(R))
+    monkeypatch.setenv("IAS_WIDE_V", "1")
+    if order == 0:
+        got, _ = ias.spgemm(R, R)
+        assert_csr_identical(got, ref, "IAS_WIDE_V=1")
+    else:
+        got_s, _ = ias.spgemm(R, R, order=ias.ORDER_SORTED)
+        np.testing.assert_array_equal(got_s.row_ptr, ref.row_ptr)
+        _check_sorted(got_s, ref, range(R.rows))
