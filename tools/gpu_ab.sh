@@ -40,7 +40,7 @@ if [ -n "$PMC_LIB" ]; then
     IAS_LIB=$PWD/build_var/libias_$PMC_LIB.so timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$n -o p -- \
        python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/pmc_$n.log 2>&1 || exit $?
   done
-  python3 tools/pmc_kernels.py $OUT "k_num2$|k_sym|k_short|k_part|k_fixup" > $OUT/pmc_summary.txt
+  python3 tools/pmc_kernels.py $OUT "k_num2(<|$)|k_sym|k_short|k_part|k_fixup" > $OUT/pmc_summary.txt
 fi
 if [ -n "$HIPTRACE" ]; then
   timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $OUT/hip -o run -- \

@@ -22,7 +22,7 @@ if [ "${PART:-a}" = a ]; then
     timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$n -o p -- \
        python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor > $OUT/pmc_$n.log 2>&1 || exit $?
   done
-  python3 tools/pmc_kernels.py $OUT "k_num2$|k_sym|k_short|k_part|k_fixup|k_expand" > $OUT/pmc_summary.txt
+  python3 tools/pmc_kernels.py $OUT "k_num2(<|$)|k_sym|k_short|k_part|k_fixup|k_expand" > $OUT/pmc_summary.txt
   python3 tools/timeline.py $OUT/prof/run_kernel_trace.csv k_an_entries -2 > $OUT/timeline_k3p.txt
   IAS_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/serial -o run --output-format csv -- \
       python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor > $OUT/serial.log 2>&1 || exit $?

@@ -26,6 +26,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
     for row in csv.DictReader(open(f)):
         k = re.sub(r"\(.*", "", row["Kernel_Name"]).replace("void ", "").replace("ias::dev::", "")
+        k = re.sub(r"^k_num2<.*>$", "k_num2", k)   # the streaming pass's instantiations (bench.py's key)
         vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
 out = {"source": sys.argv[3] if len(sys.argv) > 3 else root,
        "calibration": "read bytes = 2 x FETCH_SIZE (tools/fetch_probe.hip); WRITE_SIZE exact"}
