@@ -1361,33 +1361,58 @@ __global__ __launch_bounds__(1024) void k_scan_partials(int64_t *partial, int64_
     if (threadIdx.x == 0) partial[nb] = carry;
 }
 
+// Thread t of a tile scans its SCAN_ITEMS consecutive entries in registers
+// (two 16-byte loads when they are in range and aligned), the tile's thread
+// sums are scanned once, and the results leave through LDS in lane order (an
+// 8-byte lane each, 512 contiguous bytes per wave instruction).  The
+// item-by-item form it replaces waited on one load and two barriers per item
+// (K3' 72 us for 21 M entries, 3.5 TB/s).  LDS slot of entry e: e + e / 8
+// (two dwords of padding per thread's run: 2-way bank conflicts at most).
+static_assert(SCAN_ITEMS == 8, "k_scan_apply: two 16-byte loads per thread");
 __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_apply(const int32_t *in, int64_t n,
                                                            const int64_t *partial,
                                                            int64_t *out) {
+    __shared__ int64_t st[SCAN_TILE + SCAN_TILE / SCAN_ITEMS];
     __shared__ int64_t wsum[SCAN_BLOCK / WAVE];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
-    int64_t carry = partial[blockIdx.x];
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        const int64_t k = base + (int64_t)i * SCAN_BLOCK + threadIdx.x;
-        const int64_t v = k < n ? in[k] : 0;
-        int64_t x = v;
-        const int l = threadIdx.x & (WAVE - 1);
-        for (int d = 1; d < WAVE; d <<= 1) {
-            const int64_t t = __shfl_up(x, d);
-            if (l >= d) x += t;
-        }
-        if (l == WAVE - 1) wsum[threadIdx.x / WAVE] = x;
-        __syncthreads();
-        int64_t before = 0, tot = 0;
-        for (int w = 0; w < SCAN_BLOCK / WAVE; ++w) {
-            before += (w < (int)(threadIdx.x / WAVE)) ? wsum[w] : 0;
-            tot += wsum[w];
-        }
-        if (k < n) out[k] = carry + before + x - v;
-        __syncthreads();
-        carry += tot;
+    const int t = (int)threadIdx.x, l = t & (WAVE - 1);
+    const int64_t k0 = base + (int64_t)t * SCAN_ITEMS;
+    int32_t v[SCAN_ITEMS];
+    if (k0 + SCAN_ITEMS <= n && ((uintptr_t)in & 15u) == 0) {
+        const int4 a = *(const int4 *)(in + k0), b = *(const int4 *)(in + k0 + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < SCAN_ITEMS; ++j) v[j] = k0 + j < n ? in[k0 + j] : 0;
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = partial[gridDim.x];
+    int64_t run = 0;
+    int64_t loc[SCAN_ITEMS];
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) {
+        loc[j] = run;
+        run += v[j];
+    }
+    int64_t x = run;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+        const int64_t u = __shfl_up(x, d);
+        if (l >= d) x += u;
+    }
+    if (l == WAVE - 1) wsum[t / WAVE] = x;
+    __syncthreads();
+    int64_t before = partial[blockIdx.x] + x - run;
+#pragma unroll
+    for (int w = 0; w < SCAN_BLOCK / WAVE; ++w) before += w < t / WAVE ? wsum[w] : 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_ITEMS; ++j) st[t * (SCAN_ITEMS + 1) + j] = before + loc[j];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        const int e = i * SCAN_BLOCK + t;
+        if (base + e < n) out[base + e] = st[e + e / SCAN_ITEMS];
+    }
+    if (blockIdx.x == gridDim.x - 1 && t == 0) out[n] = partial[gridDim.x];
 }
 
 __global__ void k_shift(int64_t *p, int64_t n, int64_t off) {
