@@ -1330,33 +1330,45 @@ __global__ __launch_bounds__(SCAN_BLOCK) void k_scan_reduce(const int32_t *in, i
     }
 }
 
-// single block: exclusive scan of partial[0..nb) in place; total -> partial[nb]
+// single block: exclusive scan of partial[0..nb) in place; total -> partial[nb].
+// Eight consecutive partials per thread (a chunk of 8,192 per pass: K3''s
+// 10,234 tiles in two passes instead of ten, three barriers each).
 __global__ __launch_bounds__(1024) void k_scan_partials(int64_t *partial, int64_t nb) {
+    constexpr int PT = 8;
     __shared__ int64_t wsum[16];
-    __shared__ int64_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t b0 = 0; b0 < nb; b0 += 1024) {
-        const int64_t k = b0 + threadIdx.x;
-        const int64_t v = k < nb ? partial[k] : 0;
-        int64_t x = v;
-        const int l = threadIdx.x & (WAVE - 1);
+    const int l = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+    int64_t carry = 0;
+    for (int64_t b0 = 0; b0 < nb; b0 += 1024 * PT) {
+        const int64_t k0 = b0 + (int64_t)threadIdx.x * PT;
+        int64_t v[PT], run = 0;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) v[j] = k0 + j < nb ? partial[k0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const int64_t t = v[j];
+            v[j] = run;
+            run += t;
+        }
+        int64_t x = run;
+#pragma unroll
         for (int d = 1; d < WAVE; d <<= 1) {
             const int64_t t = __shfl_up(x, d);
             if (l >= d) x += t;
         }
-        if (l == WAVE - 1) wsum[threadIdx.x / WAVE] = x;
+        if (l == WAVE - 1) wsum[w] = x;
         __syncthreads();
         int64_t before = 0, tot = 0;
+#pragma unroll
         for (int i = 0; i < 16; ++i) {
-            before += (i < (int)(threadIdx.x / WAVE)) ? wsum[i] : 0;
+            before += i < w ? wsum[i] : 0;
             tot += wsum[i];
         }
-        const int64_t c = carry;
-        if (k < nb) partial[k] = c + before + x - v;
-        __syncthreads();
-        if (threadIdx.x == 0) carry = c + tot;
-        __syncthreads();
+        const int64_t b = carry + before + x - run;
+#pragma unroll
+        for (int j = 0; j < PT; ++j)
+            if (k0 + j < nb) partial[k0 + j] = b + v[j];
+        __syncthreads();   // wsum is rewritten by the next pass
+        carry += tot;
     }
     if (threadIdx.x == 0) partial[nb] = carry;
 }
