@@ -358,7 +358,11 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
     // rank shards of K4 run one at a time, bench.py --as-rank all; round 5:
     // 1.39 ns per row, 7.6 / 18.2 / 33.6 ps per product of the three classes;
     // DESIGN.md §6), so the rank holding R-MAT's hub rows gets fewer.
-    constexpr int64_t ROW_COST = 1830, SMALL = 10, MID = 24, BIG = 44, MID_MIN = 16384, BIG_MIN = 32768;
+    // When C's columns fit the column bitmap (CBM_MAX_COLS), every row beyond
+    // 16,384 products takes k_sym_cbm instead (serial K3': 0.55 ms for 27.5 M
+    // products, ~20 ps per product: CBM).
+    constexpr int64_t ROW_COST = 1830, SMALL = 10, MID = 24, BIG = 44, CBM = 26, MID_MIN = 16384, BIG_MIN = 32768;
+    const bool cbm = b->cols <= CBM_MAX_COLS;
     std::vector<int64_t> pref((size_t)a->rows + 1, 0);
     for (int64_t i = 0; i < a->rows; ++i) {
         int64_t prod = 0;
@@ -366,7 +370,7 @@ extern "C" ias_status ias_partition_rows(const ias_csr *A, const ias_csr *B, int
             const int32_t j = a->col[p];
             prod += b->row_ptr[j + 1] - b->row_ptr[j];
         }
-        const int64_t w = ROW_COST + prod * (prod > BIG_MIN ? BIG : prod > MID_MIN ? MID : SMALL);
+        const int64_t w = ROW_COST + prod * (prod <= MID_MIN ? SMALL : cbm ? CBM : prod > BIG_MIN ? BIG : MID);
         pref[(size_t)i + 1] = pref[(size_t)i] + w;
     }
     const int64_t total = pref[(size_t)a->rows];

@@ -38,6 +38,10 @@ void set_last_diag(uint32_t flags);   // ias_last_diag() of the calling thread
 
 inline bool is_device(int32_t memory) { return memory == IAS_MEMORY_DEVICE; }
 
+// C columns up to which the symbolic pass's longest rows take the LDS column
+// bitmap (k_sym_cbm; spgemm.hip's CBM_MAXW words of 32 columns)
+constexpr int64_t CBM_MAX_COLS = 36096ll * 32;
+
 // Shape/pointer sanity of a CSR operand (no element scan).
 ias_status check_csr_host(const ias_csr *A);
 

@@ -171,7 +171,9 @@ const char *ias_last_error(void);
  * bits 1 = the column-bitmap symbolic's minima table in global memory,
  * 2 = its duplicates found by a sweep instead of the list, 4 = its first-touch
  * words in global memory; 0 = no forcing), the OR of the IAS_DIAG_CBM_*
- * branches its rows took; 0 otherwise.  No reference counterpart. */
+ * branches its rows took; 0 otherwise, and 0 after a call that stopped
+ * before the end of its symbolic pass (an error, or no CSR product).  No
+ * reference counterpart. */
 uint32_t    ias_last_diag(void);
 #define IAS_DIAG_CBM_GLOBAL_OWN    1u   /* minima table in the row's work space */
 #define IAS_DIAG_CBM_UNLISTED_KEEP 2u   /* duplicate sweep, duplicates kept for the fix-ups */

@@ -216,7 +216,16 @@ static inline uint64_t ora_mix(uint64_t row, uint64_t pos, uint64_t col, uint64_
     return x ^ (x >> 32);
 }
 
-void ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest) {
+static int ora_cmp_i32(const void *x, const void *y) {
+    const int32_t a = *(const int32_t *)x, b = *(const int32_t *)y;
+    return (a > b) - (a < b);
+}
+
+/* sorted = 0: the reference's order (reverse discovery); 1: every row by
+ * ascending column (IAS_ORDER_SORTED, the cuSPARSE-like order of
+ * GPU/detail/cusparse/common_cusparse.h:78-91) — same sums, positions by
+ * column. */
+static void csr_digest(const ora_csr *A, const ora_csr *B, int sorted, int64_t *row_nnz, uint64_t *digest) {
     const int64_t cols = B->cols;
     uint64_t total = 0;
 #pragma omp parallel reduction(+ : total)
@@ -237,8 +246,9 @@ void ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz
                     else acc[k] = acc[k] + prod;
                 }
             }
+            if (sorted) qsort(disc, (size_t)nd, sizeof(int32_t), ora_cmp_i32);
             for (int64_t t = 0; t < nd; ++t) {
-                const int32_t k = disc[nd - 1 - t];
+                const int32_t k = sorted ? disc[t] : disc[nd - 1 - t];
                 uint64_t vb;
                 memcpy(&vb, &acc[k], sizeof vb);
                 total += ora_mix((uint64_t)i, (uint64_t)t, (uint64_t)(uint32_t)k, vb);
@@ -249,6 +259,13 @@ void ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz
         free(acc); free(seen); free(disc);
     }
     *digest = total;
+}
+
+void ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest) {
+    csr_digest(A, B, 0, row_nnz, digest);
+}
+void ora_csr_mul_csr_digest_sorted(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest) {
+    csr_digest(A, B, 1, row_nnz, digest);
 }
 
 /* ------------------------------------------------------------------ sizes */

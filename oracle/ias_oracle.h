@@ -77,6 +77,8 @@ void    ora_csr_mul_csr(const ora_csr *A, const ora_csr *B, ora_csr *C);
 /* CSR_MUL_CSR folded into per-row nnz and an order-sensitive digest of C
    (row, position, column, value bits), without storing C (full-size pins) */
 void    ora_csr_mul_csr_digest(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest);
+/* the same digest of C with every row sorted by column (IAS_ORDER_SORTED) */
+void    ora_csr_mul_csr_digest_sorted(const ora_csr *A, const ora_csr *B, int64_t *row_nnz, uint64_t *digest);
 int     ora_csr_to_coo(const ora_csr *A, ora_coo *out, double gate);
 void    ora_coo_mul_coo(const ora_coo *A, const ora_coo *B, ora_coo *C);
 int     ora_csr_to_ell(const ora_csr *A, ora_ell *out, double gate);

@@ -34,6 +34,10 @@ CASES = {
 }
 
 
+# configurations whose sorted-order digest is recorded too
+SORTED = {"rmat12_ef16_s1", "k2_ell1048576_k16_s7", "k3p_rmat20_ef20_s2"}
+
+
 def make(kind, args):
     return {"rmat": ias.gen_rmat, "band": ias.gen_band, "ell": ias.gen_ell}[kind](*args)
 
@@ -60,6 +64,8 @@ if __name__ == "__main__":
         rec["nnz_c"] = int(rp[-1])
         rec["c_row_ptr_sha256"] = hashlib.sha256(rp.tobytes()).hexdigest()
         rec["c_digest"] = dg
+        if name in SORTED:   # the IAS_ORDER_SORTED pin (tests/test_fullsize.py)
+            _, rec["c_digest_sorted"] = ob.csr_mul_csr_digest(ob.Mat.of(A), ob.Mat.of(A), sorted_rows=True)
         out[name] = rec
         print(name, rec, f"{time.time() - t:.1f}s", flush=True)
         with open(path, "w") as f:

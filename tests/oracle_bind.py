@@ -56,6 +56,7 @@ for name, res, args in [
     ("ora_flops", C.c_int64, [P(OCsr), P(OCsr)]),
     ("ora_csr_mul_csr", None, [P(OCsr), P(OCsr), P(OCsr)]),
     ("ora_csr_mul_csr_digest", None, [P(OCsr), P(OCsr), i64p, C.POINTER(C.c_uint64)]),
+    ("ora_csr_mul_csr_digest_sorted", None, [P(OCsr), P(OCsr), i64p, C.POINTER(C.c_uint64)]),
     ("ora_csr_to_coo", C.c_int, [P(OCsr), P(OCoo), C.c_double]),
     ("ora_coo_mul_coo", None, [P(OCoo), P(OCoo), P(OCoo)]),
     ("ora_csr_to_ell", C.c_int, [P(OCsr), P(OEll), C.c_double]),
@@ -134,12 +135,14 @@ def csr_mul_csr(A: Mat, B: Mat) -> Mat:
     return _take_csr(c)
 
 
-def csr_mul_csr_digest(A: Mat, B: Mat):
-    """(row_ptr of C, digest) of CSR_MUL_CSR without storing C (see tests/fulldigest.py)."""
+def csr_mul_csr_digest(A: Mat, B: Mat, sorted_rows: bool = False):
+    """(row_ptr of C, digest) of CSR_MUL_CSR without storing C (see tests/fulldigest.py);
+    sorted_rows: the digest of C with every row sorted by column (IAS_ORDER_SORTED)."""
     a, b = A.struct(), B.struct()
     nnz = np.zeros(A.rows, np.int64)
     d = C.c_uint64(0)
-    lib.ora_csr_mul_csr_digest(C.byref(a), C.byref(b), nnz.ctypes.data_as(i64p), C.byref(d))
+    f = lib.ora_csr_mul_csr_digest_sorted if sorted_rows else lib.ora_csr_mul_csr_digest
+    f(C.byref(a), C.byref(b), nnz.ctypes.data_as(i64p), C.byref(d))
     rp = np.zeros(A.rows + 1, np.int64)
     np.cumsum(nnz, out=rp[1:])
     return rp, int(d.value)

@@ -61,3 +61,29 @@ def test_digest_adds_over_row_blocks():
     # without the global row index the blocks do not add up
     s, e = int(rp[700]), int(rp[A.rows])
     assert digest_torch(rp[:701], col[:s], val[:s]) + digest_torch(rp[700:], col[s:e], val[s:e]) != want
+
+
+@pytest.mark.parametrize("A", [ias.gen_rmat(12, 16, seed=1), ias.gen_ell(8192, 16, seed=7)], ids=["rmat12", "ell8k"])
+def test_sorted_digest_matches_sorted_oracle(A):
+    """ora_csr_mul_csr_digest_sorted (the IAS_ORDER_SORTED pin of
+    test_fullsize_sorted_row_pointer) = the digest of the materialised oracle C
+    with each row sorted by column, and differs from the reference-order digest."""
+    M = ob.Mat.of(A)
+    ref = ob.csr_mul_csr(M, M)
+    col, val = ref.col.copy(), ref.val.copy()
+    for i in range(A.rows):
+        s, e = int(ref.row_ptr[i]), int(ref.row_ptr[i + 1])
+        o = np.argsort(col[s:e], kind="stable")
+        col[s:e], val[s:e] = col[s:e][o], val[s:e][o]
+    rp, dg = ob.csr_mul_csr_digest(M, M, sorted_rows=True)
+    np.testing.assert_array_equal(rp, ref.row_ptr)
+    assert digest_numpy(ref.row_ptr, col, val) == dg
+    assert dg != ob.csr_mul_csr_digest(M, M)[1]
+
+
+def test_recorded_sorted_digest_small():
+    """the recorded c_digest_sorted of the small R-MAT case reproduces"""
+    import json, os
+    rec = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "generator_stats.json")))["rmat12_ef16_s1"]
+    A = ias.gen_rmat(*rec["args"])
+    assert ob.csr_mul_csr_digest(ob.Mat.of(A), ob.Mat.of(A), sorted_rows=True)[1] == rec["c_digest_sorted"]

@@ -122,17 +122,21 @@ def test_fullsize_against_oracle(torch_dev, name, via):
         torch.cuda.empty_cache()
 
 
-def test_fullsize_sorted_row_pointer(torch_dev):
-    """IAS_ORDER_SORTED at full size (K3'): same row pointer, every row ascending,
-    and the same multiset per row (digest of the sorted oracle rows is not
-    recorded, so values are checked through the per-row sums of the hub rows)."""
+@pytest.mark.parametrize("name", ["k2_ell1048576_k16_s7", "k3p_rmat20_ef20_s2"])
+def test_fullsize_sorted_row_pointer(torch_dev, name):
+    """IAS_ORDER_SORTED at full size (K2, K3'): same row pointer, every row
+    ascending, and the order-sensitive digest of C equal to the oracle's with
+    every row sorted by column (c_digest_sorted: the cuSPARSE-like order of
+    GPU/detail/cusparse/common_cusparse.h:78-91, values bit for bit); plus the
+    hub rows entry by entry."""
     torch = torch_dev
-    rec = STATS["k3p_rmat20_ef20_s2"]
+    rec = STATS[name]
     A = make(rec)
     c_rp, c_ci, c_va, _ = device_spgemm(torch, A, order=ias.ORDER_SORTED)
     try:
         rp = c_rp.cpu().numpy()
         assert hashlib.sha256(rp.tobytes()).hexdigest() == rec["c_row_ptr_sha256"]
+        assert digest_torch(c_rp, c_ci, c_va) == rec["c_digest_sorted"], "sorted C differs from the oracle (digest)"
         # ascending inside every row: a descent may only happen at a row start
         d = (c_ci[1:] <= c_ci[:-1]).nonzero().flatten() + 1
         starts = torch.from_numpy(rp[1:-1]).to(d.device)

@@ -12,5 +12,6 @@ git worktree add -f --detach $WT $REV > /dev/null
 make -C $WT/ia-spgemm_amd -j8 libias.so > /dev/null 2>&1
 mkdir -p build_var
 cp $WT/ia-spgemm_amd/libias.so build_var/libias_$NAME.so
+echo "REV $(git rev-parse $REV)" > build_var/libias_$NAME.src   # the variant's source: that revision
 git worktree remove --force $WT
 echo "build_var/libias_$NAME.so <- $(git rev-parse --short $REV)"
