@@ -80,6 +80,8 @@ def parse(argv=None):
     p.add_argument("--gather-reps", type=int, default=1, help="N>1: repetitions of the allgatherv measurement")
     p.add_argument("--no-anchor", action="store_true",
                    help="N>1: skip timing the whole matrix on rank 0's GPU alone after the distributed loop")
+    p.add_argument("--no-weak-anchor", action="store_true",
+                   help="N=1 auto: skip timing the K4 family's N=1 point (R-MAT 2^20, ef 24, seed 3)")
     p.add_argument("--no-one-shot", action="store_true",
                    help="N=1: skip the library-allocated one-shot calls (ias_csr_mul_csr, device C)")
     return p.parse_args(argv)
@@ -95,6 +97,27 @@ def workload(cfg: str, world: int):
             f"R-MAT 2^{scale}, edge factor 24, seed 3, (a,b,c)=(.45,.15,.15): K4 family (N=8: BASELINE K4)")
     kind, prm, desc = CONFIGS[cfg]
     return kind, dict(prm), desc
+
+
+def series(cfg: str, world: int) -> dict:
+    """How this line belongs to a scaling series (config.family / scaling /
+    series): `auto` is the north-star K3' at N = 1 and the K4 family (R-MAT
+    2^(20+log2 N), edge factor 24, seed 3, ~2^20 rows per GPU) for N > 1 — a
+    weak-scaling series whose own N = 1 point (R-MAT 2^20, ef 24, seed 3) the
+    N = 1 line carries as `weak_anchor`; a named --config is the same matrix
+    for every N, a strong-scaling series."""
+    if cfg == "auto":
+        if world <= 1:
+            return {"family": "K3'", "scaling": "weak",
+                    "series": "N=1 headline: K3' (north-star). The N>1 lines are the K4-family weak-scaling "
+                              "series (R-MAT 2^(20+log2 N), ef 24, seed 3); its N=1 point is this line's "
+                              "weak_anchor"}
+        return {"family": "K4", "scaling": "weak",
+                "series": f"K4-family weak scaling: R-MAT 2^{20 + int(round(math.log2(world)))} on {world} GPUs "
+                          f"(~2^20 rows per GPU); its N=1 point is the N=1 line's weak_anchor, not its value (K3')"}
+    name = cfg.upper().replace("P", "'")
+    return {"family": name, "scaling": "strong",
+            "series": f"{name} strong scaling: the same matrix for every N, rows sharded by estimated cost"}
 
 
 def generate(kind, prm):
@@ -142,6 +165,7 @@ def main(argv=None):
     as_ranks = as_rank_list(args.as_rank, world_req) if not dist_on else None
 
     kind, prm, desc = workload(args.config, world_req)
+    ser = series(args.config, world_req)
     # ---------------- inputs: rank 0 generates, B replicated by broadcast
     t_gen = time.time()
     meta = torch.zeros(4, dtype=torch.int64)
@@ -319,12 +343,14 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": ser["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (deterministic R-MAT/band/ELL generator, ia-spgemm_amd/csrc/gen.cpp)",
             "config": {
                 "workload": desc,
+                "family": ser["family"],
+                "series": ser["series"],
                 "kind": kind, **prm,
                 "rows": rows, "nnz_a": nnz_a, "flops": flops_total, "nnz_c": nnz_c_total,
                 "order": args.order,
@@ -392,6 +418,12 @@ def main(argv=None):
                                       out["ms_per_step"], flops_total)
             if rank == 0:
                 out["same_matrix_1gpu"] = anchor
+        if rank == 0 and world == 1 and as_ranks is None and args.config == "auto" and not args.no_weak_anchor:
+            # the K4 family's N = 1 point (the weak-scaling series' anchor)
+            del cbufs, step
+            step = cbufs = None
+            torch.cuda.empty_cache()
+            out["weak_anchor"] = weak_anchor(local, dev, args.steps, args.warmup)
         if rank == 0 and world == 1 and as_ranks is None and not args.no_one_shot:
             # C's buffers go back to torch's cache, not to the driver: the
             # one-shot call then allocates fresh memory beside them, as a caller
@@ -436,6 +468,58 @@ def main(argv=None):
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def weak_anchor(local, dev, steps, warmup):
+    """The K4 family at N = 1 (R-MAT 2^20, edge factor 24, seed 3) on this GPU,
+    the same two-phase step as the line's own: the point the driver's
+    1/2/4/8-GPU curve (whose N > 1 lines are this family) scales from."""
+    import torch
+    import ias
+    kind, prm, _ = workload("auto", 2)
+    prm = dict(prm, scale=20)
+    A = generate(kind, prm)
+    flops = ias.flops(A, A)
+    rp = torch.from_numpy(A.row_ptr).to(dev)
+    ci = torch.from_numpy(A.col).to(dev)
+    va = torch.from_numpy(A.val).to(dev)
+
+    def csr(r, c, v, rows, nnz):
+        return ias.Csr(rows, A.cols, nnz, C.cast(C.c_void_p(r.data_ptr()), ias.i64p),
+                       C.cast(C.c_void_p(c.data_ptr()), ias.i32p),
+                       C.cast(C.c_void_p(v.data_ptr()), ias.f64p), ias.MEMORY_DEVICE, local)
+
+    Am = csr(rp, ci, va, A.rows, A.nnz)
+    plan = C.c_void_p()
+    ias.check(ias.lib.ias_plan_create(C.byref(plan), local, None), "plan")
+    try:
+        n = C.c_int64(0)
+        ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Am), C.byref(n), None, None), "nnz")
+        nnz = int(n.value)
+        c_rp = torch.empty(A.rows + 1, dtype=torch.int64, device=dev)
+        c_ci = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+        c_va = torch.empty(max(nnz, 1), dtype=torch.float64, device=dev)
+        Cm = csr(c_rp, c_ci, c_va, A.rows, nnz)
+
+        def step():
+            m = C.c_int64(0)
+            ias.check(ias.lib.ias_csr_mul_csr_nnz(plan, C.byref(Am), C.byref(Am), C.byref(m), None, None), "nnz")
+            ias.check(ias.lib.ias_csr_mul_csr_compute(plan, C.byref(Am), C.byref(Am), C.byref(Cm), 0, None),
+                      "compute")
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / steps
+    finally:
+        ias.lib.ias_plan_destroy(plan)
+    return {"what": "the K4 family's N=1 point: R-MAT 2^20, edge factor 24, seed 3, (a,b,c)=(.45,.15,.15) on "
+                    "this GPU, the same two-phase step",
+            "scale": 20, "ef": prm["ef"], "seed": prm["seed"], "flops": flops, "nnz_c": nnz,
+            "ms_per_step": round(ms, 4), "value": round(2.0 * flops / (ms * 1e6), 3), "steps": steps}
 
 
 def same_matrix_1gpu(plan, Afull, Bm, rows, cols, local, dev, rank, ms_dist, flops_total, steps=2):

@@ -17,7 +17,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     # name = lib or lib+VAR=value (an environment variant of a library)
     lib=${name%%+*}; envv=; [ "$lib" != "$name" ] && envv=${name#*+}
     env ${envv//+/ } IAS_LIB=$PWD/build_var/libias_$lib.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline \
-       --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/ab_${name}_$rep.json 2> $OUT/ab_${name}_$rep.err || exit $?
+       --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor $BENCH_ARGS > $OUT/ab_${name}_$rep.json 2> $OUT/ab_${name}_$rep.err || exit $?
     echo "$name $rep $(python3 -c "import json;d=json.load(open('$OUT/ab_${name}_$rep.json'));print(d['value'],d['ms_per_step'],d['phases_ms_rank0'],d['roofline'].get('ms_per_launch'))")" >> $S
   done
 done
@@ -25,20 +25,20 @@ cat $S
 if [ -n "$SERIAL_LIB" ]; then
   IAS_SERIAL=1 IAS_LIB=$PWD/build_var/libias_$SERIAL_LIB.so timeout -k 10 300 rocprofv3 --kernel-trace --stats \
      -d $OUT/serial -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
-     --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/serial.log 2>&1 || exit $?
+     --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor $BENCH_ARGS > $OUT/serial.log 2>&1 || exit $?
   python3 tools/kstats.py $OUT/serial/run_kernel_stats.csv 7 > $OUT/serial_kstats.txt
 fi
 if [ -n "$TRACE_LIB" ]; then
   IAS_LIB=$PWD/build_var/libias_$TRACE_LIB.so timeout -k 10 300 rocprofv3 --kernel-trace --stats \
      -d $OUT/trace -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline \
-     --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/trace.log 2>&1 || exit $?
+     --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor $BENCH_ARGS > $OUT/trace.log 2>&1 || exit $?
   python3 tools/timeline.py $OUT/trace/run_kernel_trace.csv k_an_entries -2 > $OUT/timeline.txt
 fi
 if [ -n "$PMC_LIB" ]; then
   for c in "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS" FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
     n=$(echo $c | cut -d' ' -f1)
     IAS_LIB=$PWD/build_var/libias_$PMC_LIB.so timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$n -o p -- \
-       python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor $BENCH_ARGS > $OUT/pmc_$n.log 2>&1 || exit $?
+       python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor $BENCH_ARGS > $OUT/pmc_$n.log 2>&1 || exit $?
   done
   python3 tools/pmc_kernels.py $OUT "k_num2(<|$)|k_sym|k_short|k_part|k_fixup" > $OUT/pmc_summary.txt
 fi
