@@ -668,7 +668,7 @@ extern "C" ias_status ias_csr_mul_csr(const ias_csr *A, const ias_csr *B, ias_cs
     dev::Rows rb{dB->row_ptr, nullptr, 0, dB->col, dB->val};
     ias_csr D{};
     plan->last_a = plan->last_b = nullptr;
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep, dB->nnz));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, dA->nnz, rep));
     const int64_t nnz = plan->nnz_total;
     IAS_TRY(ias_csr_alloc(&D, A->rows, B->cols, nnz, IAS_MEMORY_DEVICE, plan->device));
     HIPC(hipMemcpyAsync(D.row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
@@ -728,7 +728,7 @@ extern "C" ias_status ias_coo_mul_coo(const ias_coo *A, const ias_coo *B, ias_co
     if (rep && !st.owned.empty()) rep->ms_upload = host_ms() - t_up;
     dev::Rows ra{ap, nullptr, 0, ac, av};
     dev::Rows rb{bp, nullptr, 0, bc, bv};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep, B->nnz));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
     const int64_t nnz = plan->nnz_total;
     ias_coo D{};
     D.rows = A->rows; D.cols = B->cols; D.nnz = nnz; D.memory = IAS_MEMORY_DEVICE;
@@ -802,7 +802,7 @@ extern "C" ias_status ias_ell_mul_ell(const ias_ell *A, const ias_ell *B, ias_el
     if (rep && !st.owned.empty()) rep->ms_upload = host_ms() - t_up;
     dev::Rows ra{nullptr, an, A->max_nnz_per_row, ac, av};
     dev::Rows rb{nullptr, bn, B->max_nnz_per_row, bc, bv};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, (int64_t)ak, rep, (int64_t)bk));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, (int64_t)ak, rep));
     const int32_t K = plan->max_nnz;
     ias_ell D{};
     D.rows = A->rows; D.cols = B->cols; D.nnz = plan->nnz_total; D.max_nnz_per_row = K;
@@ -885,7 +885,7 @@ extern "C" ias_status ias_csr_mul_csr_nnz(ias_plan *plan, const ias_csr *A, cons
     if (rep) memset(rep, 0, sizeof *rep);
     dev::Rows ra{A->row_ptr, nullptr, 0, A->col, A->val};
     dev::Rows rb{B->row_ptr, nullptr, 0, B->col, B->val};
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep, B->nnz));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
     plan->last_a = A->col;
     plan->last_b = B->col;
     *nnz_c = plan->nnz_total;
@@ -947,7 +947,7 @@ extern "C" ias_status ias_csr_mul_csr_into(ias_plan *plan, const ias_csr *A, con
     C->cols = B->cols;
     int64_t nnz = 0;
     // the two-phase engine behind one call: nnz, then values when they fit
-    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep, B->nnz));
+    IAS_TRY(plan->symbolic(ra, rb, A->rows, B->cols, A->nnz, rep));
     nnz = plan->nnz_total;
     HIPC(hipMemcpyAsync(C->row_ptr, plan->bufs[ias_plan::B_PTR].p, sizeof(int64_t) * (A->rows + 1),
                         hipMemcpyDeviceToDevice, s));

@@ -37,8 +37,6 @@ constexpr int N2_WPB = 4;      // waves (units) per workgroup
 struct Num2Unit {
     int32_t row;
     int32_t e0;   // first A entry of the unit within the row
-    int32_t n;    // A entries (<= N2_ENT)
-    int32_t pad;
 };
 
 struct Num2Args {
@@ -53,12 +51,6 @@ struct Num2Args {
     Bitmap bm;
     const int64_t *dup_off;
     double *dupval;
-    // B-slice queues (null: units [0, nunits) in order): workgroup b takes
-    // queue b % 8 of this launch's class, position (b / 8) * N2_WPB + wave —
-    // the workgroups of one queue share an XCD (round-robin dispatch), so
-    // each XCD's L2 holds the B rows of its own slices (k_n2_split)
-    const int64_t *qoff;     // 25 offsets: queue (cls, x) = [qoff[8 cls + x], qoff[8 cls + x + 1])
-    int32_t cls;
 };
 
 // Units: every streaming row with products gets ceil(entries / 64) of them,
@@ -81,7 +73,7 @@ __global__ void k_num2_count(Rows A, int64_t rows, const int32_t *dupn, const in
 }
 // uoff: exclusive scan of cnt[0 .. 3*rows] (uoff[3*rows] = all units); thread 0
 // also stores the unit count and the class boundaries in the counters
-__global__ void k_num2_fill(Rows A, int64_t rows, const int32_t *cnt, const int64_t *uoff, Num2Unit *units,
+__global__ void k_num2_fill(int64_t rows, const int32_t *cnt, const int64_t *uoff, Num2Unit *units,
                             Counters *tot) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
@@ -92,12 +84,8 @@ __global__ void k_num2_fill(Rows A, int64_t rows, const int32_t *cnt, const int6
     if (i >= 3 * rows) return;
     const int32_t c = cnt[i];
     const int64_t o = uoff[i];
-    if (c == 0) return;
     const int32_t r = (int32_t)(i % rows);
-    int64_t as;
-    int32_t an;
-    A.row(r, as, an);
-    for (int32_t j = 0; j < c; ++j) units[o + j] = Num2Unit{r, j * N2_ENT, min(N2_ENT, an - j * N2_ENT), 0};
+    for (int32_t j = 0; j < c; ++j) units[o + j] = Num2Unit{r, j * N2_ENT};
 }
 
 // 16-byte non-temporal store (C is not read back by this pass)
@@ -139,16 +127,8 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     static_assert((PASS + 4) * 4 % 16 == 0 && (PASS + 2) * 8 % 16 == 0, "16-byte aligned staging rows");
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / WAVE));
     const int lane = (int)(threadIdx.x & (WAVE - 1));
-    int64_t u;
-    if (a.qoff) {
-        const int g = (int)(blockIdx.x & 7u);
-        const int64_t qs = a.qoff[8 * a.cls + g], qe = a.qoff[8 * a.cls + g + 1];
-        u = qs + (int64_t)(blockIdx.x >> 3) * N2_WPB + w;
-        if (u >= qe) return;
-    } else {
-        u = (int64_t)blockIdx.x * N2_WPB + w;
-        if (u >= a.nunits) return;
-    }
+    const int64_t u = (int64_t)blockIdx.x * N2_WPB + w;
+    if (u >= a.nunits) return;
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -160,7 +140,7 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
     int32_t an;
     a.A.row(row, as, an);
     const int64_t q0 = as - a.A.base() + un.e0;
-    const int32_t n = un.n;
+    const int32_t n = min(N2_ENT, an - un.e0);
     const int64_t prow = a.poff[row];
     // this lane's entry
     int32_t bl = 0, rel = 0;
@@ -335,188 +315,6 @@ __global__ __launch_bounds__(64 * N2_WPB) __attribute__((amdgpu_waves_per_eu(N2_
         store(pw0, s1);
         pw0 += PASS;
         if (pw0 >= pb) break;
-    }
-}
-
-// ---------------------------------------------------------------- B slices
-// (round 6)  Every product of the streaming pass gathers its B row's column
-// and value; B (K3': 250 MB) is ~60x an XCD's 4 MB L2, and with units in row
-// order every XCD sweeps all of B over the whole pass, so nearly every gather
-// goes past L2 (a trace-driven L2 model of K3''s units: hit rate 0.09, 14.3
-// GB past L2 per pass against 10.4 GB gathered — the counters' 15.9 GB).
-// Units are cut where their entries' B rows cross one of P = 8 S slices of
-// B's entry space holding equal products; slice p goes to queue x = p % 8
-// (one XCD) at sweep s = p / 8, and each queue is ordered by sweep, so at
-// any time an XCD gathers from about 1/P of B.  A cut unit is still a
-// contiguous range of its row's A entries, so its products and its C entries
-// stay contiguous and k_num2 needs no change beyond the queue lookup.
-constexpr int N2_NBK = 2048;        // weight buckets over B's entry space
-constexpr int N2_SAMP = 8;          // the weights sample one 64-entry chunk of A in 8
-constexpr int N2_MAXP = 64;         // slices
-constexpr int N2_SPLIT_WPB = 16;    // base units per workgroup of k_n2_split
-
-// Products per bucket of B's entry space, from a sample of A's entries
-// (their B rows' lengths at their B rows' starts).
-__global__ __launch_bounds__(1024) void k_n2_hist(AxView ax, int64_t a_entries, const int64_t *bptr, int shift,
-                                                  unsigned long long *hist) {
-    __shared__ unsigned long long h[N2_NBK];
-    for (int i = threadIdx.x; i < N2_NBK; i += blockDim.x) h[i] = 0ull;
-    __syncthreads();
-    const int64_t bbase = bptr ? bptr[0] : 0;   // B's first entry (CSR views), 0 for ELL
-    const int64_t nchunk = (a_entries + WAVE - 1) / WAVE;
-    const int64_t wv = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / WAVE;
-    const int64_t nw = (int64_t)gridDim.x * blockDim.x / WAVE;
-    const int lane = (int)(threadIdx.x & (WAVE - 1));
-    for (int64_t c = wv * N2_SAMP; c < nchunk; c += nw * N2_SAMP) {
-        const int64_t q = c * WAVE + lane;
-        if (q < a_entries) {
-            const int32_t bl = ax.blen[q];
-            if (bl > 0) {
-                const int64_t b = (ax.bstart[q] - bbase) >> shift;
-                atomicAdd(&h[b < 0 ? 0 : (b >= N2_NBK ? N2_NBK - 1 : b)], (unsigned long long)bl);
-            }
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < N2_NBK; i += blockDim.x)
-        if (h[i]) atomicAdd(&hist[i], h[i]);
-}
-
-// Slice bounds in B's entry space: bnd[p] (p = 1 .. P-1) is the end of the
-// bucket where the products' prefix reaches p/P of the total; one workgroup
-// of 1024 threads, two buckets each.  Clears the histogram for the next call.
-__global__ __launch_bounds__(1024) void k_n2_bnd(unsigned long long *hist, int P, const int64_t *bptr, int shift,
-                                                 int64_t *bnd) {
-    __shared__ unsigned long long ws[1024 / WAVE];
-    const int t = threadIdx.x, lane = t & (WAVE - 1), w = t / WAVE;
-    const unsigned long long h0 = hist[2 * t], h1 = hist[2 * t + 1];
-    hist[2 * t] = 0ull;
-    hist[2 * t + 1] = 0ull;
-    // inclusive scan of h0 + h1 over the threads
-    unsigned long long x = h0 + h1;
-#pragma unroll
-    for (int d = 1; d < WAVE; d <<= 1) {
-        const unsigned long long y = __shfl_up(x, d);
-        if (lane >= d) x += y;
-    }
-    if (lane == WAVE - 1) ws[w] = x;
-    __syncthreads();
-    unsigned long long before = 0, tot = 0;
-    for (int i = 0; i < 1024 / WAVE; ++i) {
-        before += i < w ? ws[i] : 0ull;
-        tot += ws[i];
-    }
-    const unsigned long long incl1 = before + x, incl0 = incl1 - h1, excl0 = incl0 - h0;
-    const int64_t bbase = bptr ? bptr[0] : 0;
-    if (t == 0) {
-        bnd[0] = INT64_MIN;
-        bnd[P] = INT64_MAX;
-    }
-    if (tot == 0) {   // no products: everything in slice 0
-        for (int p = 1 + t; p < P; p += 1024) bnd[p] = INT64_MAX;
-        return;
-    }
-    // target of bound p: ceil(p * tot / P); bucket i takes the targets in (excl, incl]
-    for (int p = 1; p < P; ++p) {
-        const unsigned long long tg = ((unsigned long long)p * tot + (unsigned long long)P - 1ull) / (unsigned long long)P;
-        if (tg > excl0 && tg <= incl0) bnd[p] = bbase + ((int64_t)(2 * t + 1) << shift);
-        else if (tg > incl0 && tg <= incl1) bnd[p] = bbase + ((int64_t)(2 * t + 2) << shift);
-    }
-}
-
-struct N2Split {
-    const Num2Unit *base;                 // 64-entry units, by class (k_num2_fill)
-    const Counters *cnt;                  // n2_units, n2_bunits, n2_dunits
-    Rows A;
-    AxView ax;
-    const int64_t *bnd;                   // P + 1 slice bounds (k_n2_bnd)
-    int32_t P, S;                         // P = 8 S
-    int64_t nblk;                         // workgroups of the split kernels
-    int32_t *kcnt;                        // count pass: sub-units per (key, workgroup), key-major
-    const int64_t *koff;                  // fill pass: exclusive scan of kcnt
-    Num2Unit *sub;                        // fill pass: the sub-units
-};
-
-// Cut every base unit where its entries' slice changes: a wave per base
-// unit, a lane per entry; a cut starts at a non-empty entry whose slice
-// differs from the previous non-empty entry's (the first sub-unit also takes
-// the unit's leading empty entries, the last its trailing ones).  Key of a
-// sub-unit: (class, queue x = p % 8, sweep s = p / 8), key-major counts per
-// workgroup; the fill pass recomputes them and places each sub-unit at its
-// key's offset + its slot (an LDS counter: any order within a workgroup's
-// key is a valid order).
-template <bool FILL>
-__global__ __launch_bounds__(WAVE * N2_SPLIT_WPB) void k_n2_split(N2Split a) {
-    __shared__ int64_t bnd[N2_MAXP + 1];
-    __shared__ int32_t hist[3 * N2_MAXP];
-    const int P = a.P;
-    for (int i = threadIdx.x; i <= P; i += blockDim.x) bnd[i] = a.bnd[i];
-    for (int i = threadIdx.x; i < 3 * P; i += blockDim.x) hist[i] = 0;
-    __syncthreads();
-    const int w = (int)(threadIdx.x / WAVE), lane = (int)(threadIdx.x & (WAVE - 1));
-    const int64_t nb = (int64_t)a.cnt->n2_units;
-    const int64_t u = (int64_t)blockIdx.x * N2_SPLIT_WPB + w;
-    bool start = false;
-    int key = 0;
-    Num2Unit sub{};
-    if (u < nb) {
-        const Num2Unit un = a.base[u];
-        int64_t as;
-        int32_t an;
-        a.A.row(un.row, as, an);
-        const int64_t q0 = as - a.A.base() + un.e0;
-        int32_t bl = 0;
-        int p = 0;
-        if (lane < un.n) {
-            bl = a.ax.blen[q0 + lane];
-            const int64_t bs = a.ax.bstart[q0 + lane];
-            // slice: the largest p with bnd[p] <= bs
-            int lo = 0, hi = P;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (bnd[mid] <= bs) lo = mid;
-                else hi = mid;
-            }
-            p = lo;
-        }
-        const uint64_t ne = __ballot(bl > 0);
-        const uint64_t below = ne & ((1ull << lane) - 1ull);
-        const int prev = below ? 63 - __clzll((long long)below) : -1;
-        const int pp = __shfl(p, prev < 0 ? 0 : prev);
-        start = bl > 0 && (prev < 0 || pp != p);
-        const uint64_t sm = __ballot(start);
-        if (start) {
-            const uint64_t after = sm & ~((2ull << lane) - 1ull);
-            const int next = after ? __ffsll((long long)after) - 1 : un.n;
-            const int first = (sm & ((1ull << lane) - 1ull)) ? lane : 0;
-            sub = Num2Unit{un.row, un.e0 + first, next - first, 0};
-            const int cls = u < (int64_t)a.cnt->n2_bunits ? 0 : (u < (int64_t)a.cnt->n2_dunits ? 1 : 2);
-            key = (cls * 8 + (p & 7)) * a.S + (p >> 3);
-        }
-    }
-    int slot = 0;
-    if (start) slot = atomicAdd(&hist[key], 1);
-    __syncthreads();
-    if constexpr (!FILL) {
-        for (int k = threadIdx.x; k < 3 * P; k += blockDim.x) a.kcnt[(int64_t)k * a.nblk + blockIdx.x] = hist[k];
-    } else {
-        if (start) a.sub[a.koff[(int64_t)key * a.nblk + blockIdx.x] + slot] = sub;
-    }
-}
-
-// Queue bounds from the scanned key counts (qoff[8 cls + x] = first sub-unit
-// of key (cls, x, 0); qoff[24] = all) and each class's longest queue (the
-// launch grids, read by the host with the counters).
-__global__ void k_n2_qoff(const int64_t *koff, int32_t S, int64_t nblk, int64_t *qoff, Counters *c) {
-    __shared__ int64_t q[25];
-    const int t = threadIdx.x;
-    if (t < 25) q[t] = koff[(int64_t)t * S * nblk];
-    __syncthreads();
-    if (t < 25) qoff[t] = q[t];
-    if (t < 3) {
-        int64_t m = 0;
-        for (int x = 0; x < 8; ++x) m = max(m, q[8 * t + x + 1] - q[8 * t + x]);
-        c->n2_q[t] = (unsigned long long)m;
     }
 }
 

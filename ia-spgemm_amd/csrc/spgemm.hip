@@ -2646,62 +2646,9 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     return IAS_SUCCESS;
 }
 
-// IAS_N2_SLICES (read per call): B slices of the streaming pass's queues,
-// a multiple of 8 up to N2_MAXP; 0 / unset: N2_SLICES_DEF (0: units in row
-// order, one queue)
-constexpr int N2_SLICES_DEF = 0;
-static int n2_slices_env() {
-    const char *e = getenv("IAS_N2_SLICES");
-    return e && *e ? atoi(e) : N2_SLICES_DEF;
-}
-
-// The streaming pass's units cut by B slice into 8 queues of sweeps (see
-// num2_kernels.hpp, k_n2_split): sampled product weights over B's entry
-// space, slice bounds, a count pass, a scan of the key-major counts, a fill
-// pass and the queue bounds — all on `s`, before the counters' read-back
-// (which carries each class's longest queue: the launch grids).
-ias_status ias_plan::n2_slice(const Rows &A, const Rows &B, int64_t rows, int64_t a_entries, hipStream_t s) {
-    int P = n2_slices_env();
-    if (P < 8 || b_entries <= 0 || small || a_entries <= 0) return IAS_SUCCESS;
-    P = std::min(N2_MAXP, P / 8 * 8);
-    const int S = P / 8;
-    int shift = 0;
-    while (((b_entries + (1ll << shift) - 1) >> shift) > N2_NBK) ++shift;
-    const int64_t nbase = rows + a_entries / N2_ENT + 1;   // base units: B_N2UNIT's bound
-    const int64_t nblk = (nbase + N2_SPLIT_WPB - 1) / N2_SPLIT_WPB;
-    const int64_t nkeys = 3 * (int64_t)P * nblk;
-    const int64_t nparts = (nkeys + SCAN_TILE - 1) / SCAN_TILE;
-    IAS_TRY(reserve(B_N2KCNT, sizeof(int32_t) * (size_t)nkeys));
-    IAS_TRY(reserve(B_N2KOFF, sizeof(int64_t) * (size_t)(nkeys + 1 + nparts + 8)));
-    // a sub-unit starts at a non-empty entry or at its base unit's first
-    const int64_t nsub = std::min<int64_t>(a_entries + nbase, nbase * (int64_t)P);
-    IAS_TRY(reserve(B_N2SUB, sizeof(Num2Unit) * (size_t)nsub));
-    IAS_TRY(reserve(B_N2Q, sizeof(uint64_t) * (size_t)(N2_NBK + N2_MAXP + 1 + 32)));
-    unsigned long long *hist = as<unsigned long long>(bufs[B_N2Q]);
-    int64_t *bnd = (int64_t *)(hist + N2_NBK);
-    int64_t *qoff = bnd + N2_MAXP + 1;
-    int32_t *kcnt = as<int32_t>(bufs[B_N2KCNT]);
-    int64_t *koff = as<int64_t>(bufs[B_N2KOFF]);
-    Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
-    const AxView ax = ax_view();
-    HIPC(hipMemsetAsync(hist, 0, sizeof(uint64_t) * N2_NBK, s));
-    k_n2_hist<<<64, 1024, 0, s>>>(ax, a_entries, B.ptr, shift, hist);
-    k_n2_bnd<<<1, 1024, 0, s>>>(hist, P, B.ptr, shift, bnd);
-    const N2Split sp{as<Num2Unit>(bufs[B_N2UNIT]), dc2, A, ax, bnd, P, S, nblk, kcnt, koff,
-                     as<Num2Unit>(bufs[B_N2SUB])};
-    k_n2_split<false><<<(unsigned)nblk, WAVE * N2_SPLIT_WPB, 0, s>>>(sp);
-    scan_i32(kcnt, nkeys, koff + nkeys + 1, koff, s);
-    k_n2_split<true><<<(unsigned)nblk, WAVE * N2_SPLIT_WPB, 0, s>>>(sp);
-    k_n2_qoff<<<1, 64, 0, s>>>(koff, S, nblk, qoff, dc2);
-    CHECK_LAUNCH("k_n2_split", s);
-    n2_slices = P;
-    return IAS_SUCCESS;
-}
-
 ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_t cols,
-                              int64_t a_entries, ias_report *rep, int64_t b_span) {
+                              int64_t a_entries, ias_report *rep) {
     n_cols = cols;
-    b_entries = b_span;
     set_last_diag(0);   // ias_last_diag(): this call's branches, or none if it stops early
     IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
@@ -2973,7 +2920,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     int64_t *ptr = as<int64_t>(bufs[B_PTR]);
     IAS_TRY(reserve(B_NITEM, sizeof(PartItem) * (size_t)(rows + flops / NUM_PART_CAP + 2)));
     n2_units = n2_bunits = n2_dunits = 0;
-    n2_slices = 0;
     if (rows > 0) {
         k_scan_reduce<<<(unsigned)nb, SCAN_BLOCK, 0, s>>>(nnz, rows, as<int64_t>(bufs[B_PART]),
                                                           &dc2->max_nnz);
@@ -3004,10 +2950,9 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             int64_t *uoff = as<int64_t>(bufs[B_N2OFF]);
             k_num2_count<<<grid_for(rows, 256), 256, 0, s>>>(A, rows, sa.dupn, as<int32_t>(bufs[B_PROD]), cnt);
             scan_i32(cnt, 3 * rows, as<int64_t>(bufs[B_PART]), uoff, s);
-            k_num2_fill<<<grid_for(3 * rows, 256), 256, 0, s>>>(A, rows, cnt, uoff, as<Num2Unit>(bufs[B_N2UNIT]),
+            k_num2_fill<<<grid_for(3 * rows, 256), 256, 0, s>>>(rows, cnt, uoff, as<Num2Unit>(bufs[B_N2UNIT]),
                                                                  dc2);
             CHECK_LAUNCH("k_num2_fill", s);
-            IAS_TRY(n2_slice(A, B, rows, a_entries, s));
         }
     } else {
         HIPC(hipMemsetAsync(ptr, 0, sizeof(int64_t), s));
@@ -3031,7 +2976,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     n2_units = (int64_t)c2.n2_units;
     n2_bunits = (int64_t)c2.n2_bunits;
     n2_dunits = (int64_t)c2.n2_dunits;
-    for (int k = 0; k < 3; ++k) n2_q[k] = (int64_t)c2.n2_q[k];
     if (c2.overflow) {
         set_last_error("hash partition table overflow in the symbolic pass");
         return IAS_ERROR_OVERFLOW;
@@ -3178,23 +3122,14 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                 // units by class: [0, bunits) rows with > 1024 duplicates,
                 // [bunits, dunits) with fewer, [dunits, units) without
                 const int64_t cut[4] = {0, fix_split ? n2_bunits : 0, fix_split ? n2_dunits : 0, n2_units};
-                const bool sliced = n2_slices > 0;
                 for (int k = 0; k < 3; ++k) {
-                    // sliced: the class's eight B-slice queues (always one
-                    // launch per class; grid = 8 x the longest queue's workgroups)
-                    const int64_t nu = sliced ? n2_q[k] : cut[k + 1] - cut[k];
+                    const int64_t nu = cut[k + 1] - cut[k];
                     if (nu > 0) {
                         Num2Args nk = na;
-                        if (sliced) {
-                            nk.units = as<Num2Unit>(bufs[B_N2SUB]);
-                            nk.qoff = (const int64_t *)(as<unsigned long long>(bufs[B_N2Q]) + N2_NBK) + N2_MAXP + 1;
-                            nk.cls = k;
-                        } else {
-                            nk.units += cut[k];
-                            nk.nunits = nu;
-                        }
+                        nk.units += cut[k];
+                        nk.nunits = nu;
                         if (rep) HIPC(hipEventRecord(n2_ev[2 * k], t));
-                        const unsigned g = (unsigned)((nu + N2_WPB - 1) / N2_WPB) * (sliced ? 8u : 1u);
+                        const unsigned g = (unsigned)((nu + N2_WPB - 1) / N2_WPB);
                         if (wide_v) {
                             if (out.order == 0) k_num2<true, 0><<<g, 64 * N2_WPB, 0, t>>>(nk, out);
                             else k_num2<true, 1><<<g, 64 * N2_WPB, 0, t>>>(nk, out);

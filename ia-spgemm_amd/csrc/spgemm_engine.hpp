@@ -46,7 +46,6 @@ struct Counters {
     unsigned long long nnz_total;           // nnz(C) (k_bin_count of the numeric binning)
     long long a_base;                       // A's first entry (row_ptr[0]; k_an_rows)
     unsigned long long n2_units, n2_bunits, n2_dunits;   // k_num2_fill: all units, class ends
-    unsigned long long n2_q[3];                          // k_n2_qoff: longest B-slice queue per class
     int32_t max_prod;
     int32_t max_nnz;
     int32_t overflow;
@@ -69,8 +68,6 @@ struct ias_plan {
         B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
         // work units of the row-unit numeric pass (num2)
         B_N2CNT, B_N2OFF, B_N2UNIT,
-        // B-slice queues of the streaming pass: key counts + their scan, sub-units, bounds
-        B_N2KCNT, B_N2KOFF, B_N2SUB, B_N2Q,
         // sym3's retry lists (rows whose possible-duplicate list overflowed)
         B_S3RETRY,
         // k_sym_gtab's global tables (keys, own) for the two bins beyond SYM2_MAX
@@ -119,9 +116,6 @@ struct ias_plan {
     int64_t n2_units = 0;   // work units of the row-unit numeric pass
     int64_t n2_bunits = 0;  //   of which the first belong to rows with > 1024 duplicates,
     int64_t n2_dunits = 0;  //   and up to here to rows with duplicates
-    int32_t n2_slices = 0;  // B slices of the streaming pass's queues (0: units in row order)
-    int64_t n2_q[3] = {};   //   longest queue per class
-    int64_t b_entries = 0;  // B's entry span (symbolic's argument; 0: unknown, no slices)
     hipEvent_t fix_ev[2] = {}; // units of class 0 / class 1 done: their fix-ups may start
     hipEvent_t n2_ev[6] = {};  // around each streaming-pass launch: ms_stream = their sum
     // symbolic stream balancing fed back from the previous call: each bin's
@@ -152,13 +146,9 @@ struct ias_plan {
     ias_status analysis_launch(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
                                int64_t a_entries);
     const double *ax_aval = nullptr;   // A.val + the view's base (set after the analysis read-back)
-    // b_entries: B's stored entries (CSR: nnz of the view; ELL: rows * width)
     ias_status symbolic(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows,
-                        int64_t cols, int64_t a_entries, ias_report *rep, int64_t b_entries = 0);
+                        int64_t cols, int64_t a_entries, ias_report *rep);
     ias::dev::AxView ax_view();
-    // cut the streaming pass's units by B slice into per-XCD queues (IAS_N2_SLICES)
-    ias_status n2_slice(const ias::dev::Rows &A, const ias::dev::Rows &B, int64_t rows, int64_t a_entries,
-                        hipStream_t s);
     ias_status numeric(const ias::dev::Rows &A, const ias::dev::Rows &B, const ias::dev::Out &out,
                        ias_report *rep);
 };
