@@ -731,6 +731,13 @@ struct CbmArgs {
     int32_t own_cap;   // LDS words beyond the bitmap + prefixes (the minima table when it fits)
     int32_t force;     // test knob (IAS_CBM_FORCE): CBM_NO_LIST / CBM_NO_LWORDS force those branches
     uint32_t *hits;    // test knob: the branches the rows took (CBM_HIT_*, OR-ed), or nullptr
+    // column slices (k_sym_cbm<true>, C wider than one bitmap): slices per
+    // row, the rows listed, each row's work-space cursor (zeroed) and the
+    // duplicate pairs' list (k_dup_place places them)
+    int32_t nslice;
+    int32_t nrows;
+    unsigned long long *wcur;
+    uint2 *gpairs;
 };
 // IAS_CBM_FORCE bits (own_cap = 0 forces the global minima table) and the
 // branch flags k_sym_cbm ORs into CbmArgs::hits
@@ -752,18 +759,41 @@ __device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// SL (round 6): C wider than one LDS bitmap (K4: 8.4 M columns).  One
+// workgroup per (row, column slice of 32 * ncw columns): the passes above
+// restricted to the products whose column falls in the slice (every sweep
+// reads the row's whole expansion, L2-resident: a row's slices share an XCD
+// and run together), the slice's part of the row's work space reserved by a
+// count pass, the duplicate bits cleared in the row's global first-touch
+// words (preset to all ones by k_expand_flat), nnz and the duplicate pairs
+// added to the row's (k_bitmap_prefix and k_dup_place finish, as for the
+// hash partitions).  No hash partitions, no bucket pass.
+template <bool SL>
 __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t cbm[];
     __shared__ int scratch[64];
     __shared__ int ncnt[3];
+    __shared__ unsigned long long sl_base[2];
     const int NCW = a.ncw;
     uint32_t *spre = cbm + NCW;
-    const RowRef ref = a.list[blockIdx.x];
+    // SL: workgroup b -> (row index, slice); the slices of a row are b, b + 8,
+    // ... (one XCD by the dispatcher's round robin, its L2 keeps the row's
+    // expansion), eight rows interleaved
+    int32_t ridx = (int32_t)blockIdx.x, slice = 0;
+    if constexpr (SL) {
+        const int32_t per = 8 * a.nslice;
+        const int32_t g = (int32_t)blockIdx.x / per, rem = (int32_t)blockIdx.x % per;
+        slice = rem / 8;
+        ridx = g * 8 + rem % 8;
+        if (ridx >= a.nrows) return;
+    }
+    const RowRef ref = a.list[ridx];
     const int32_t row = ref.row;
     const int32_t P = ref.n;
+    const int32_t cbase = slice * 32 * NCW;   // the slice's first column
     const int tid = (int)threadIdx.x, lane = tid & (WAVE - 1);
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t *wk = (uint32_t *)(a.work + ref.q0);   // 2 P words
+    uint32_t *wk = (uint32_t *)(a.work + ref.q0);   // 2 P words (SL: 2 PS words of them, below)
     Timer tmr;   // phases (IAS_TIMING builds): 0 pass 1, 1 multi bitmap, 2 ranks, 3 pass 2, 4 pass 3, 5 prefixes, 6 placement
     tmr.start();
     for (int i = tid; i < NCW / 4; i += CBM_BLOCK) ((uint4 *)cbm)[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -774,13 +804,18 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     // next block's loads issued before this block's work (2U in flight)
     constexpr int U = CBM_U;
     const int32_t *tc = a.tcol + ref.q0;
+    // SL: columns relative to the slice; a product of another slice reads as
+    // -1 and takes no part (insl)
+    const uint32_t sw = 32u * (uint32_t)NCW;
     auto load = [&](int32_t b0, int32_t(&c)[U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int32_t p = b0 + u * CBM_BLOCK + tid;
             c[u] = p < P ? tc[p] : 0;
+            if constexpr (SL) c[u] = p < P && (uint32_t)(c[u] - cbase) < sw ? c[u] - cbase : -1;
         }
     };
+    auto insl = [&](int32_t c) -> bool { return !SL || c >= 0; };
     // blockwise: work(b0, c) gets U columns per lane (products b0 + u *
     // CBM_BLOCK + tid), so its LDS operations are issued U at a time
     auto sweep = [&](auto &&work) {
@@ -825,18 +860,34 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         }
         return at;
     };
+    // SL: the slice's products (PS) and its 2 PS words of the row's work space
+    int32_t PS = P;
+    if constexpr (SL) {
+        int cnt = 0;
+        sweep([&](int32_t b0, const int32_t(&c)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) cnt += (b0 + u * CBM_BLOCK + tid < P && c[u] >= 0) ? 1 : 0;
+        });
+        int tot;
+        (void)Team<CBM_BLOCK>::excl_sum(cnt, tot, scratch);
+        PS = tot;
+        if (tid == 0) sl_base[0] = PS > 0 ? atomicAdd(&a.wcur[ridx], 2ull * (unsigned long long)PS) : 0ull;
+        __syncthreads();
+        if (PS == 0) return;
+        wk += sl_base[0];
+    }
     // ---- 1. distinct columns; the duplicates list their column
     sweep([&](int32_t b0, const int32_t(&c)[U]) {
         uint32_t old[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             old[u] = 0u;
-            if (b0 + u * CBM_BLOCK + tid < P) old[u] = atomicOr(&cbm[c[u] >> 5], 1u << (c[u] & 31));
+            if (b0 + u * CBM_BLOCK + tid < P && insl(c[u])) old[u] = atomicOr(&cbm[c[u] >> 5], 1u << (c[u] & 31));
         }
         bool dup[U];
         int at[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) dup[u] = (old[u] >> (c[u] & 31)) & 1u;
+        for (int u = 0; u < U; ++u) dup[u] = insl(c[u]) && ((old[u] >> (c[u] & 31)) & 1u);
         append(dup, at, 0);
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -845,12 +896,19 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     __syncthreads();
     tmr.mark(0);
     const int32_t nd = ncnt[0];
-    const int32_t nnz = P - nd;
+    const int32_t nnz = PS - nd;
     const int32_t W = (P + 31) >> 5;
     uint32_t *gbits = a.bm.bits + a.bm.off[row];
     uint32_t *gpref = a.bm.pref + a.bm.off[row];
     const int32_t cap = a.div > 0 ? min(P / a.div, a.dmax) : 0;
-    const bool keep = nd <= cap;
+    // SL: the slice's pairs go to the row's list at a reserved offset (the
+    // row's count, dupn, decides the path in k_dup_place); kept while they fit
+    bool keep = nd <= cap;
+    if constexpr (SL) {
+        if (tid == 0) sl_base[1] = (nd > 0 && cap > 0) ? (unsigned long long)atomicAdd(&a.dupn[row], nd) : 0ull;
+        __syncthreads();
+        keep = cap > 0 && (int64_t)sl_base[1] + nd <= cap;
+    }
     int M = 0;   // columns of more than one product
     uint2 *pairs = nullptr;   // the duplicates (product, first touch) when kept
     bool lwords = false;      // first-touch words in LDS (over the dead column bitmap)
@@ -923,13 +981,13 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         // order, one above the column's current minimum issues no atomic (a
         // hub column's later products do not queue on one L2 address).
         const int32_t m0 = OL ? 0 : (M + 1) & ~1;
-        const int32_t mcap = (2 * P - m0) / 2;
+        const int32_t mcap = (2 * PS - m0) / 2;
         uint2 *ml = (uint2 *)(wk + m0);
         sweep([&](int32_t b0, const int32_t(&c)[U]) {
             bool on[U];
             uint32_t r[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) on[u] = b0 + u * CBM_BLOCK + tid < P && multi(c[u]);
+            for (int u = 0; u < U; ++u) on[u] = b0 + u * CBM_BLOCK + tid < P && insl(c[u]) && multi(c[u]);
             // ranks of the multi products only: their superblocks' loads
             // first (masked to those lanes, all in flight), then the sums
             uint4 x[U], y[U];
@@ -965,16 +1023,16 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
         tmr.mark(3);
         // ---- 4. duplicates: clear their first-touch bits, list (product, first touch)
         const int32_t nml = ncnt[2];
-        const bool listed = !(a.force & CBM_NO_LIST) && nml + (keep ? nd : 0) <= mcap;   // + room for the pairs
-        pairs = (uint2 *)(wk + (listed ? m0 + 2 * nml : m0));
-        lwords = listed && W <= NCW && !(a.force & CBM_NO_LWORDS);
+        const bool listed = !(a.force & CBM_NO_LIST) && nml + ((keep && !SL) ? nd : 0) <= mcap;   // + room for the pairs
+        pairs = SL ? a.gpairs + a.dup_off[row] + sl_base[1] : (uint2 *)(wk + (listed ? m0 + 2 * nml : m0));
+        lwords = !SL && listed && W <= NCW && !(a.force & CBM_NO_LWORDS);
         hit = (OL ? CBM_HIT_LDS_OWN : CBM_HIT_GLOBAL_OWN) | (lwords ? 0u : CBM_HIT_GLOBAL_WORDS) |
               (listed ? (keep ? CBM_HIT_LISTED_KEEP : CBM_HIT_LISTED_DROP)
                       : (keep ? CBM_HIT_UNLISTED_KEEP : CBM_HIT_UNLISTED_DROP));
         if (lwords) {
             for (int32_t i = tid; i < W; i += CBM_BLOCK) cbm[i] = full_word(i);
             __syncthreads();
-        } else {
+        } else if (!SL) {   // SL: preset by k_expand_flat (the row's slices share the words)
             for (int32_t i = tid; i < W; i += CBM_BLOCK) gbits[i] = full_word(i);
             __syncthreads();
         }
@@ -1017,7 +1075,7 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
                     const int32_t p = b0 + u * CBM_BLOCK + tid;
                     uint32_t f = 0u;
                     bool dup = false;
-                    if (p < P && multi(c[u])) {
+                    if (p < P && insl(c[u]) && multi(c[u])) {
                         const uint32_t r = rank(c[u]);
                         f = OL ? own[r] : ld_agent(&own[r]);
                         dup = f != (uint32_t)p;
@@ -1044,6 +1102,13 @@ __global__ __launch_bounds__(CBM_BLOCK) void k_sym_cbm(CbmArgs a) {
     }
     __syncthreads();
     tmr.mark(4);
+    if constexpr (SL) {   // prefixes and placement: k_bitmap_prefix, k_dup_place
+        if (tid == 0) {
+            atomicAdd(&a.nnz_row[row], nnz);
+            if (a.hits && hit) atomicOr(a.hits, hit);
+        }
+        return;
+    }
     // ---- words (from the LDS, or all ones without duplicates) and their
     // prefixes, tiles of CBM_BLOCK words, carried
     auto word = [&](int32_t i) -> uint32_t {
@@ -1938,9 +2003,19 @@ __global__ __launch_bounds__(256) void k_expand_part(Rows A, AxView ax, const in
 // over the lanes' starts — so every gather slot carries a product and each
 // window's stores are one contiguous run (R-MAT's B rows hold ~20 - 30
 // entries: a wave per entry left half its lanes idle).
+// words (k_sym_cbm<true>: the sliced rows) non-null: it also presets each
+// row's first-touch words to all ones (its products; the slices clear their
+// duplicates' bits).
 __global__ __launch_bounds__(256) void k_expand_flat(Rows A, AxView ax, const int64_t *axp, const int64_t *poff,
-                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol) {
+                                                     const RowRef *list, const int32_t *bcol, int32_t *tcol,
+                                                     Bitmap words) {
     const RowRef ref = list[blockIdx.x];
+    if (words.bits && blockIdx.y == 0) {
+        uint32_t *g = words.bits + words.off[ref.row];
+        const int32_t W = (ref.n + 31) >> 5;
+        for (int32_t i = (int32_t)threadIdx.x; i < W; i += (int32_t)blockDim.x)
+            g[i] = (i < W - 1 || (ref.n & 31) == 0) ? ~0u : ((1u << (ref.n & 31)) - 1u);
+    }
     int64_t s;
     int32_t n;
     A.row(ref.row, s, n);
@@ -2078,6 +2153,20 @@ static bool cbm_enabled() {
         return !(e && *e == '0');
     }();
     return on;
+}
+// Column slices of the column-bitmap symbolic when C is wider than one bitmap
+// (k_sym_cbm<true>), up to CBS_MAXS of them, with IAS_SYM_CBS=1 (read per
+// call); otherwise the hash partitions.  Opt-in: on K4 (8 slices) every slice
+// sweeps its row's whole expansion, and the slices measured slower than the
+// hash partitions (whole-K4 symbolic 59.1 vs 42.0 ms)
+// Slices of 2^20 columns (32,768 words): 3,968 LDS minima slots beside the
+// bitmap, as for a 2^20-column C; K4's 2^23 columns are 8 slices
+constexpr int32_t CBS_MAXS = 16;
+constexpr int32_t CBS_W = 32768;   // bitmap words per slice
+static int32_t cbs_slices(int64_t cols) { return (int32_t)((cols + 32ll * CBS_W - 1) / (32ll * CBS_W)); }
+static bool cbs_on(int64_t cols) {
+    const char *e = getenv("IAS_SYM_CBS");
+    return cbm_enabled() && e && *e == '1' && cbs_slices(cols) <= CBS_MAXS;
 }
 
 // LDS bins: upper bound of the key and kernel configuration; table slots
@@ -2694,6 +2783,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // fit it (k_sym_cbm), else hash partitions (expansion + buckets)
     const int32_t ncw = cbm_words(cols);
     const bool cbm = cbm_path;
+    const bool cbs = !cbm_path && cbs_on(cols);
     IAS_TRY(reserve(B_TCOL, sizeof(int32_t) * (size_t)std::max<int64_t>((int64_t)c1.part_prod, 1)));
     const int32_t *tcol = as<int32_t>(bufs[B_TCOL]);
 
@@ -2797,14 +2887,38 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
             const int32_t own_lds = (int32_t)std::max<int64_t>(0, ((int64_t)160 * 1024 - 512 - (int64_t)cbm_lds_bytes(ncw)) / 4);
             const int32_t own_cap = (force & CBM_GLOBAL_OWN) ? 0 : own_lds;
             const size_t lds = cbm_lds_bytes(ncw) + 4ull * own_lds;
-            allow_lds(k_sym_cbm, cbm_done, lds);
+            allow_lds(k_sym_cbm<false>, cbm_done, lds);
             k_expand_flat<<<dim3((unsigned)c, 4), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
-                                                               as<int32_t>(bufs[B_TCOL]));
+                                                               as<int32_t>(bufs[B_TCOL]), Bitmap{});
             const CbmArgs ca{tcol, SL + st[sym_part], ncw, as<uint2>(bufs[B_PBKT]), bm, nnz,
                              sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, own_cap, force,
-                             fe && *fe ? (uint32_t *)&dc2->cbm_hits : nullptr};
-            k_sym_cbm<<<c, CBM_BLOCK, lds, t>>>(ca);
+                             fe && *fe ? (uint32_t *)&dc2->cbm_hits : nullptr, 1, c, nullptr, nullptr};
+            k_sym_cbm<false><<<c, CBM_BLOCK, lds, t>>>(ca);
             CHECK_LAUNCH("k_sym_cbm", t);
+        } else if (cbs) {
+            // wider C (round 6): the same passes per column slice of 2^20
+            // columns, a workgroup per (row, slice)
+            static bool cbs_done = false;
+            const char *fe = getenv("IAS_CBM_FORCE");
+            const int32_t force = fe && *fe ? (int32_t)atoi(fe) : 0;
+            const int32_t own_lds = (int32_t)std::max<int64_t>(0, ((int64_t)160 * 1024 - 512 - (int64_t)cbm_lds_bytes(CBS_W)) / 4);
+            const int32_t own_cap = (force & CBM_GLOBAL_OWN) ? 0 : own_lds;
+            const size_t lds = cbm_lds_bytes(CBS_W) + 4ull * own_lds;
+            allow_lds(k_sym_cbm<true>, cbs_done, lds);
+            IAS_TRY(reserve(B_CBSCUR, sizeof(unsigned long long) * (size_t)c));
+            unsigned long long *wcur = as<unsigned long long>(bufs[B_CBSCUR]);
+            HIPC(hipMemsetAsync(wcur, 0, sizeof(unsigned long long) * (size_t)c, t));
+            k_expand_flat<<<dim3((unsigned)c, 4), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
+                                                               as<int32_t>(bufs[B_TCOL]), bm);
+            const CbmArgs ca{tcol, SL + st[sym_part], CBS_W, as<uint2>(bufs[B_PBKT]), bm, nnz,
+                             sa.dup_off, sa.dupn, sa.dupt, PART_DCAP_DIV, FIXBIG_CAP, own_cap, force,
+                             fe && *fe ? (uint32_t *)&dc2->cbm_hits : nullptr, cbs_slices(cols), c, wcur,
+                             as<uint2>(bufs[B_DUPP])};
+            k_sym_cbm<true><<<(unsigned)((c + 7) / 8 * 8 * ca.nslice), CBM_BLOCK, lds, t>>>(ca);
+            k_bitmap_prefix<<<c, 256, 0, t>>>(SL + st[sym_part], c, as<int32_t>(bufs[B_PROD]), bm);
+            k_dup_place<<<c, 256, 0, t>>>(SL + st[sym_part], c, bm, as<uint2>(bufs[B_DUPP]), sa.dup_off, sa.dupn,
+                                          sa.dupt, PART_DCAP_DIV, FIXBIG_CAP);
+            CHECK_LAUNCH("k_sym_cbm<true>", t);
         } else {
             k_expand_part<<<dim3((unsigned)c, 8), 256, 0, t>>>(A, ax, axp, poff, SL + st[sym_part], B.col,
                                                                    as<int32_t>(bufs[B_TCOL]), SYM_PART_CAP);

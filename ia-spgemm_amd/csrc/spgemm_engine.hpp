@@ -68,6 +68,8 @@ struct ias_plan {
         B_PFIRST, B_PBOFF, B_PBKT, B_PSPAN,
         // work units of the row-unit numeric pass (num2)
         B_N2CNT, B_N2OFF, B_N2UNIT,
+        // the column-slice symbolic's per-row work-space cursors
+        B_CBSCUR,
         // sym3's retry lists (rows whose possible-duplicate list overflowed)
         B_S3RETRY,
         // k_sym_gtab's global tables (keys, own) for the two bins beyond SYM2_MAX

@@ -199,3 +199,62 @@ def test_dia_plan_cache_eviction(monkeypatch):
                                           bits(ref["val"].ravel()))
         ias.lib.ias_dia_free(C.byref(da))
         ias.lib.ias_dia_free(C.byref(dc))
+
+
+def _diag_matrix(n, offs, seed):
+    rng = np.random.default_rng(seed)
+    rows = [np.array(sorted(i + o for o in offs if 0 <= i + o < n), np.int64) for i in range(n)]
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    return ias.HostCsr(n, n, rp, col, rng.standard_normal(col.size))
+
+
+def test_dia_into_reused_plan_sees_changed_offsets(monkeypatch):
+    """ias_dia_mul_dia_into with device offsets reuses the last call's plan
+    without reading them back (dia.hip, DiaFast); the device-side check must
+    catch offsets rewritten in place between calls (same arrays, same counts):
+    each call bitwise equal to the oracle of what the arrays hold."""
+    import torch
+    monkeypatch.delenv("IAS_DIA_MFMA", raising=False)
+    n = 4096
+    mats = [_diag_matrix(n, [-3, -2, -1, 0, 1, 2, 3], 1), _diag_matrix(n, [-9, -6, -3, 0, 3, 6, 9], 2),
+            _diag_matrix(n, [-3, -2, -1, 0, 1, 2, 3], 3)]
+    dev = torch.device("cuda", 0)
+    host = []
+    for A in mats:
+        s, h = A.struct(), ias.Dia()
+        ias.check(ias.lib.ias_csr_to_dia(C.byref(s), C.byref(h), 0.0), "to_dia")
+        assert h.num_diagonals == 7
+        host.append((ias._np(h.diagonal_offsets, 7, np.int32).copy(), ias._np(h.val, n * 7, np.float64).copy(),
+                     ias._np(h.diagonal_ind, 2 * n - 1, np.int32).copy()))
+        ias.lib.ias_dia_free(C.byref(h))
+    a_off = torch.from_numpy(host[0][0]).to(dev)
+    a_val = torch.from_numpy(host[0][1]).to(dev)
+    a_ind = torch.from_numpy(host[0][2]).to(dev)
+    da = ias.Dia(rows=n, cols=n, num_diagonals=7, choice=1,
+                 diagonal_offsets=C.cast(C.c_void_p(a_off.data_ptr()), ias.i32p),
+                 diagonal_ind=C.cast(C.c_void_p(a_ind.data_ptr()), ias.i32p),
+                 val=C.cast(C.c_void_p(a_val.data_ptr()), ias.f64p), memory=ias.MEMORY_DEVICE, device=0)
+    cap = 13
+    offs = torch.zeros(cap, dtype=torch.int32, device=dev)
+    ind = torch.zeros(2 * n - 1, dtype=torch.int32, device=dev)
+    val = torch.zeros(n * cap, dtype=torch.float64, device=dev)
+    for step, k in enumerate([0, 0, 1, 1, 2, 0]):
+        a_off.copy_(torch.from_numpy(host[k][0]))
+        a_val.copy_(torch.from_numpy(host[k][1]))
+        a_ind.copy_(torch.from_numpy(host[k][2]))
+        torch.cuda.synchronize()
+        Cd = ias.Dia(rows=0, cols=0, num_diagonals=cap, choice=0,
+                     diagonal_offsets=C.cast(C.c_void_p(offs.data_ptr()), ias.i32p),
+                     diagonal_ind=C.cast(C.c_void_p(ind.data_ptr()), ias.i32p),
+                     val=C.cast(C.c_void_p(val.data_ptr()), ias.f64p), memory=ias.MEMORY_DEVICE, device=0)
+        ias.check(ias.lib.ias_dia_mul_dia_into(C.byref(da), C.byref(da), C.byref(Cd), None, None), f"into {step}")
+        torch.cuda.synchronize()
+        ref = ob.dia_mul_dia(ob.Mat.of(mats[k]), ob.Mat.of(mats[k]))
+        nd = int(Cd.num_diagonals)
+        assert nd == ref["nd"], (step, nd, ref["nd"])
+        np.testing.assert_array_equal(offs.cpu().numpy()[:nd], ref["offsets"], err_msg=f"step {step}")
+        np.testing.assert_array_equal(ind.cpu().numpy(), ref["ind"], err_msg=f"step {step}")
+        np.testing.assert_array_equal(bits(val.cpu().numpy()[:n * nd]), bits(ref["val"].ravel()),
+                                      err_msg=f"step {step}")

@@ -376,3 +376,80 @@ def test_wide_v_knob(monkeypatch, order):
         got_s, _ = ias.spgemm(R, R, order=ias.ORDER_SORTED)
         np.testing.assert_array_equal(got_s.row_ptr, ref.row_ptr)
         _check_sorted(got_s, ref, range(R.rows))
+
+
+def cbs_rows(seed=29):
+    """A*B with B 3,158,000 columns wide (four column-bitmap slices of 2^20
+    columns, the last partial: k_sym_cbm<true>) whose first A rows exceed
+    32,768 products (the rows that took the hash partitions before round 6),
+    each from B rows of 100 columns drawn from a pool — (products, pool):
+      spread over every slice, few repeated columns (LDS minima, kept);
+      40,000 columns across the slice 0 / 1 boundary (duplicates dropped);
+      5,000 columns over all slices (most products duplicates: dropped);
+      200,000 columns of slice 2 (kept);
+      10,000 columns of the partial last slice;
+      1,000 columns of slice 0 (every other slice empty for this row);
+    then 1,500 ordinary rows."""
+    rng = np.random.default_rng(seed)
+    per, ncols, sw = 100, 3_158_000, 1 << 20
+    pools = [(60000, rng.choice(ncols, 2_000_000, replace=False)),
+             (50000, np.arange(sw - 20000, sw + 20000)),
+             (40000, rng.choice(ncols, 5000, replace=False)),
+             (40000, np.arange(2 * sw, 2 * sw + 200000)),
+             (36000, np.arange(3 * sw, 3 * sw + 10000)),
+             (36000, np.arange(1000))]
+    brows, arows = [], []
+    for prods, pool in pools:
+        base = len(brows)
+        for _ in range(prods // per):
+            brows.append(rng.choice(pool, per, replace=False))
+        arows.append(np.arange(base, len(brows)))
+    nb = len(brows)
+    for _ in range(3000):
+        brows.append(rng.choice(ncols, 12, replace=False))
+    for _ in range(1500):
+        arows.append(rng.choice(np.arange(nb, len(brows)), 8, replace=False))
+    return _csr(arows, len(brows), rng), _csr(brows, ncols, rng)
+
+
+@pytest.fixture(scope="module")
+def cbs_case():
+    A, B = cbs_rows()
+    return A, B, ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+
+
+@pytest.mark.parametrize("force", [0, 1, 2, 3, "hash"], ids=["cbs", "cbs-global-own", "cbs-unlisted",
+                                                              "cbs-both", "hash-partitions"])
+def test_column_slices_wide_b(cbs_case, monkeypatch, force):
+    """Rows beyond 32,768 products on a C wider than one LDS bitmap: the
+    column-sliced k_sym_cbm<true> (opt-in, IAS_SYM_CBS=1; its first-touch
+    words always in global memory: GLOBAL_WORDS in ias_last_diag proves it
+    ran), its forced branches, and the default hash partitions — all
+    bitwise, both orders."""
+    A, B, ref = cbs_case
+    if force == "hash":
+        monkeypatch.delenv("IAS_SYM_CBS", raising=False)   # the default path
+        monkeypatch.setenv("IAS_CBM_FORCE", "0")
+    else:
+        monkeypatch.setenv("IAS_SYM_CBS", "1")
+        monkeypatch.setenv("IAS_CBM_FORCE", str(force))
+    got, rep = ias.spgemm(A, B)
+    hits = int(ias.lib.ias_last_diag())
+    assert rep.max_row_products == 60000
+    assert_csr_identical(got, ref, f"column slices, force={force}")
+    if force == "hash":
+        assert hits == 0
+    else:
+        assert hits & GLOBAL_WORDS, f"{hits:#x}"
+        if force & 1:
+            assert hits & GLOBAL_OWN and not hits & LDS_OWN
+        if force & 2:
+            assert not hits & (LISTED_KEEP | LISTED_DROP)
+        if force == 0:
+            assert hits & (LISTED_KEEP | LISTED_DROP) and hits & LDS_OWN and hits & GLOBAL_OWN
+    got_s, _ = ias.spgemm(A, B, order=ias.ORDER_SORTED)
+    for i in range(6):
+        s, e = ref.row_ptr[i], ref.row_ptr[i + 1]
+        o = np.argsort(ref.col[s:e], kind="stable")
+        np.testing.assert_array_equal(got_s.col[s:e], ref.col[s:e][o])
+        np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))

@@ -18,7 +18,7 @@ for rep in $(seq 1 ${REPS:-2}); do
     lib=${name%%+*}; envv=; [ "$lib" != "$name" ] && envv=${name#*+}
     env ${envv//+/ } IAS_LIB=$PWD/build_var/libias_$lib.so timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline \
        --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor $BENCH_ARGS > $OUT/ab_${name}_$rep.json 2> $OUT/ab_${name}_$rep.err || exit $?
-    echo "$name $rep $(python3 -c "import json;d=json.load(open('$OUT/ab_${name}_$rep.json'));print(d['value'],d['ms_per_step'],d['phases_ms_rank0'],d['roofline'].get('ms_per_launch'))")" >> $S
+    echo "$name $rep $(python3 -c "import json;d=json.load(open('$OUT/ab_${name}_$rep.json'));print(d['value'],d['ms_per_step'],d.get('phases_ms_rank0'),d.get('roofline',{}).get('ms_per_launch'))")" >> $S
   done
 done
 cat $S
