@@ -16,16 +16,16 @@ if [ "${PART:-a}" = a ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || exit $?
   timeout -k 10 500 $B > $OUT/bench_k3p.json 2> $OUT/bench_k3p.err || exit $?
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- \
-      python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-e2e --no-one-shot > $OUT/bench_k3p_rocprof.json 2> $OUT/bench_k3p_rocprof.err || exit $?
+      python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-e2e --no-one-shot --no-weak-anchor > $OUT/bench_k3p_rocprof.json 2> $OUT/bench_k3p_rocprof.err || exit $?
   for c in FETCH_SIZE WRITE_SIZE "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS" "TCC_HIT_sum TCC_MISS_sum"; do
     n=$(echo $c | cut -d' ' -f1)
     timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace --output-format csv -d $OUT/pmc_$n -o p -- \
-       python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor > $OUT/pmc_$n.log 2>&1 || exit $?
+       python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor > $OUT/pmc_$n.log 2>&1 || exit $?
   done
   python3 tools/pmc_kernels.py $OUT "k_num2(<|$)|k_sym|k_short|k_part|k_fixup|k_expand" > $OUT/pmc_summary.txt
   python3 tools/timeline.py $OUT/prof/run_kernel_trace.csv k_an_entries -2 > $OUT/timeline_k3p.txt
   IAS_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/serial -o run --output-format csv -- \
-      python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor > $OUT/serial.log 2>&1 || exit $?
+      python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-host-e2e --no-one-shot --no-anchor --no-weak-anchor > $OUT/serial.log 2>&1 || exit $?
   python3 tools/kstats.py $OUT/serial/run_kernel_stats.csv 7 > $OUT/serial_kstats_k3p.txt
 else
   timeout -k 10 600 $B --config k3 --no-host-e2e --cpu-full > $OUT/bench_k3.json 2> $OUT/bench_k3.err || exit $?

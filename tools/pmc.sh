@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p $OUT
 timeout -k 10 120 rocprofv3 -L > $OUT/counters_list.txt 2>&1
-CMD="python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
+CMD="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-weak-anchor ${BENCH_ARGS:-}"
 i=0
 while read -r group; do
   [ -z "$group" ] && continue
