@@ -2239,7 +2239,12 @@ static_assert(val_bins_covered(), "value-bin emission does not cover a bin's tab
 // the partitioned bin (k_sym_cbm); otherwise also the two bins to 32,768
 // products (sym5<32768>; K4: 4.6 vs 31.5 ps per product in the hash
 // partitions), the longer rows hash-partitioned.
-static int sym_nval(bool cbm) {
+// wide: B's selected rows end beyond 2^30 entries (32-bit offsets fail): the
+// rows beyond SYM5_MAX take the hash partitions, not the 8-wave sym5 bins
+// (whose every row would go through the global tables: K4 forced that way,
+// symbolic 115.5 ms at one workgroup per CU against 53.0 ms through the hash
+// partitions; round 6, profiles/r06/gtab/)
+static int sym_nval(bool cbm, bool wide = false) {
     static const int nv = [] {
         const char *e = getenv("IAS_SYM_CBM_MIN");
         if (!e || !*e) return N_SYM2_LDS;
@@ -2248,7 +2253,7 @@ static int sym_nval(bool cbm) {
         while (n < N_SYM2_LDS && SYM2_BINS[n].upper < v) ++n;
         return n;
     }();
-    return cbm ? (big_mode() == 2 ? N_SYM2 : nv) : (big_mode() ? N_SYM2 : N_SYM2_LDS);
+    return cbm ? (big_mode() == 2 ? N_SYM2 : nv) : (big_mode() && !wide ? N_SYM2 : N_SYM2_LDS);
 }
 
 static BinSpec sym_spec(int nval = N_SYM2) {
@@ -2461,9 +2466,18 @@ static void sym5_launch(const Sym3Args &a, hipStream_t s) {
 }
 // k_sym_gtab over a row list (device count a.retry_count), `grid`
 // workgroups each with GT_SLOTS table slots of `keys` / `own`
+// workgroups: GT_GRID_MAX for sym5's hand-backs (rare rows), GT_GRID_ALL
+// (one per CU) when every row of the bins comes here (B beyond 32-bit
+// offsets): K4 with every 16,385 - 32,768-product row forced here
+// (IAS_GTAB_ALL=1), symbolic 134.9 ms at 64 workgroups (advisor, round 5)
 constexpr int GT_GRID_MAX = 64;
-static void gtab_launch(const Sym3Args &a, int64_t grid, int32_t *keys, uint32_t *own, hipStream_t s) {
-    grid = std::max<int64_t>(1, std::min<int64_t>(grid, GT_GRID_MAX));
+constexpr int GT_GRID_ALL = 256;
+static bool gtab_all(int32_t wide_b) {   // IAS_GTAB_ALL=1: test knob, read per call
+    const char *ga = getenv("IAS_GTAB_ALL");
+    return wide_b || (ga && *ga == '1');
+}
+static void gtab_launch(const Sym3Args &a, int64_t grid, int32_t *keys, uint32_t *own, hipStream_t s, int gmax) {
+    grid = std::max<int64_t>(1, std::min<int64_t>(grid, gmax));
     k_sym_gtab<<<(unsigned)grid, GT_BLOCK, 0, s>>>(a, keys, own);
 }
 // (its retries: sym2's 1024-lane teams, cfg 7 / SYM2_CFG_WIDE)
@@ -2687,7 +2701,7 @@ ias_status ias_plan::analysis_launch(const Rows &A, const Rows &B, int64_t rows,
     n_rows = rows;
     n_entries = a_entries;
     cbm_path = cbm_words(n_cols) <= CBM_MAXW && cbm_enabled();
-    const BinSpec ss = sym_spec(sym_nval(cbm_path));
+    const BinSpec ss = sym_spec(sym_nval(cbm_path, wide_redo));
     const size_t ae = (size_t)std::max<int64_t>(a_entries, 1);
     IAS_TRY(reserve(B_AXS, sizeof(int64_t) * ae));
     IAS_TRY(reserve(B_AXL, sizeof(int32_t) * ae));
@@ -2739,6 +2753,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                               int64_t a_entries, ias_report *rep) {
     n_cols = cols;
     set_last_diag(0);   // ias_last_diag(): this call's branches, or none if it stops early
+    wide_redo = false;
     IAS_TRY(analysis_launch(A, B, rows, a_entries));
     hipStream_t s = (hipStream_t)stream;
     // the previous call's symbolic bins are done: their durations for this
@@ -2752,7 +2767,6 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
                 sym_w[b] = 1e6 * (double)ms / sym_est_prev[b];
             (void)hipGetLastError();
         }
-    const BinSpec ss = sym_spec(sym_nval(cbm_path)), ns = num_spec();
     Counters *dc = as<Counters>(bufs[B_CNT]);
     Counters *dc2 = as<Counters>(bufs[B_CNT]) + 1;
     Counters *hc = (Counters *)host_counters;
@@ -2761,6 +2775,17 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     const int64_t nb = (rows + SCAN_TILE - 1) / SCAN_TILE;
     HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));   // + A's base entry
     HIPC((hipError_t)host_wait(s));
+    bool big_rows = false;   // rows in the 8-wave sym5 bins (numbered N_SYM2_LDS + 1 ..)
+    for (int b = N_SYM2_LDS + 1; b <= N_SYM2 && sym_nval(cbm_path) == N_SYM2; ++b) big_rows |= hc->count[b] > 0;
+    if (hc->wide_b && big_rows && sym_nval(cbm_path, true) != sym_nval(cbm_path)) {
+        // B beyond 32-bit offsets: the analysis again with the bins of that
+        // case (its binning needs the flag the analysis itself raises)
+        wide_redo = true;
+        IAS_TRY(analysis_launch(A, B, rows, a_entries));
+        HIPC(hipMemcpyAsync(hc, dc, sizeof(Counters), hipMemcpyDeviceToHost, s));
+        HIPC((hipError_t)host_wait(s));
+    }
+    const BinSpec ss = sym_spec(sym_nval(cbm_path, wide_redo)), ns = num_spec();
     const Counters c1 = *hc;
     ax_aval = A.val + (rows > 0 ? c1.a_base : 0);
     const AxView ax = ax_view();
@@ -2795,7 +2820,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     IAS_TRY(reserve(B_PBKT, sizeof(uint2) * (size_t)(c1.part_prod + 1)));
     if (!c1.wide_b) IAS_TRY(reserve(B_S3RETRY, sizeof(RowRef) * (size_t)(rows + 1)));
     if (ss.nval > N_SYM2_LDS && (c1.count[N_SYM2_LDS + 1] > 0 || c1.count[N_SYM2_LDS + 2] > 0)) {
-        const size_t tab = (size_t)(N_SYM2 - N_SYM2_LDS) * GT_GRID_MAX * GT_SLOTS;
+        const size_t tab = (size_t)(N_SYM2 - N_SYM2_LDS) * (gtab_all(c1.wide_b) ? GT_GRID_ALL : GT_GRID_MAX) * GT_SLOTS;
         IAS_TRY(reserve(B_GTKEY, sizeof(int32_t) * tab));
         IAS_TRY(reserve(B_GTOWN, sizeof(uint32_t) * tab));
     }
@@ -2968,22 +2993,21 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         if (retry_feedback() && retry_prev[b & 15] >= 0 && retry_upper[b & 15] == u)
             r2.count = std::min<int32_t>(c, std::max<int32_t>(2 * retry_prev[b & 15] + 2, RETRY_GRID_MIN));
         if (u > SYM5_MAX) {   // SYM_CFG_BIG: sym5<32768>, its retries through the global tables
-            const size_t tab = (size_t)(b - N_SYM2_LDS - 1) * GT_GRID_MAX * GT_SLOTS;
+            const bool all = gtab_all(c1.wide_b);
+            const size_t tab = (size_t)(b - N_SYM2_LDS - 1) * (all ? GT_GRID_ALL : GT_GRID_MAX) * GT_SLOTS;
             int32_t *gk = as<int32_t>(bufs[B_GTKEY]) + tab;
             uint32_t *go = as<uint32_t>(bufs[B_GTOWN]) + tab;
             Sym3Args a5{ax, B.col, SL + st[b], c, as<int32_t>(bufs[B_PROD]), nnz, bm, sa.dup_off,
                         sa.dupn, sa.dupt, dcap_for(u), DW_MAX, as<RowRef>(bufs[B_S3RETRY]) + st[b],
                         &dc->s3_retry[b & 15]};
-            // IAS_GTAB_ALL=1 (test knob, read per call): the wide-B branch
-            const char *ga = getenv("IAS_GTAB_ALL");
-            if (!c1.wide_b && !(ga && *ga == '1')) {
+            if (!all) {
                 sym5_launch<GT_U, 8>(a5, t);
                 CHECK_LAUNCH("k_sym5", t);
-                gtab_launch(a5, r2.count, gk, go, t);
+                gtab_launch(a5, r2.count, gk, go, t, GT_GRID_MAX);
             } else {   // B beyond 32-bit offsets: every row of the bin through the global tables
                 a5.retry = SL + st[b];
                 a5.retry_count = &dc->count[b];
-                gtab_launch(a5, c, gk, go, t);
+                gtab_launch(a5, c, gk, go, t, GT_GRID_ALL);
             }
             CHECK_LAUNCH("k_sym_gtab", t);
             return IAS_SUCCESS;

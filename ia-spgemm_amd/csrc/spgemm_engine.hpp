@@ -107,6 +107,7 @@ struct ias_plan {
     int64_t n_cols = 0;      // C's columns
     bool cbm_path = false;   // partitioned rows: one LDS column bitmap per row (k_sym_cbm)
     bool wide_v = false;     // B entries beyond 2^29 among the selected rows (k_num2<true, …>)
+    bool wide_redo = false;  // this call's analysis redone with the bins of B beyond 2^30 entries
     int64_t n_entries = 0;   // stored entries of A (expanded-A length)
     int64_t nnz_total = 0;
     int64_t flops = 0;

@@ -329,6 +329,18 @@ def test_big_rows_wide_b(monkeypatch, force):
         np.testing.assert_array_equal(bits(got_s.val[s:e]), bits(ref.val[s:e][o]))
 
 
+def test_big_rows_beyond_32bit_offsets():
+    """The 16,385 - 32,768-product rows of a wide B whose entries sit beyond
+    2^30: the analysis is redone with those rows in the hash partitions (not
+    the global tables); bitwise."""
+    A, B = big_rows()
+    ref = ob.csr_mul_csr(ob.Mat.of(A), ob.Mat.of(B))
+    A2 = ias.HostCsr(A.rows, A.cols + 1, A.row_ptr, A.col + 1, A.val)
+    got, rep = ias.spgemm(A2, _padded_b(B, (1 << 30) + 1000))
+    assert rep.max_row_products == 830 * 40
+    assert_csr_identical(got, ref, "rows beyond 16,384 products, B beyond 2^30 entries")
+
+
 def _padded_b(B, pad):
     """B behind a first row of `pad` entries (column 0, value 0) that A never
     selects: every selected row's entries sit beyond `pad`."""
