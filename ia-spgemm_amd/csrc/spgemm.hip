@@ -2092,10 +2092,6 @@ constexpr int SYM_PART_LOG2S = 14; // table slots of a symbolic partition (2^14 
 constexpr int32_t SYM_PART_CAP = ((1 << SYM_PART_LOG2S) * 2) / 3;   // products per symbolic partition
 constexpr int32_t NUM_PART_CAP = 10922;   // nnz per numeric partition (16384-slot table)
 constexpr int32_t WIDE_MIN = (1 << 19) - 1;
-// serial ns per product of the column-bitmap symbolic with its expansion
-// (stream balancing; K3' 0.55 ms for 27.5 M products; 12 / 20 / 30 within
-// noise on K3': 9.63 / 9.60 / 9.61 ms, profiles/r04/ab/cbm_cost_ab.txt)
-constexpr double CBM_COST = 20.0;
 // IAS_SYM_CBM=0: the partitioned rows take the hash partitions (A/B)
 static bool retry_print() {
     static const bool on = [] {
@@ -2104,39 +2100,7 @@ static bool retry_print() {
     }();
     return on;
 }
-// k_fixup_big (lists > 4,096 duplicates) at the head of the fix-up stream,
-// once its rows' units are done, instead of between the streaming pass's
-// launches on the pass's stream: K3' numeric 5.16 -> 5.06 ms, K3 +0.15 ms
-// (round 5, profiles/r05/ab/fixbig_*); IAS_FIXBIG_SIDE=0: the pass's stream
-static bool part_side() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_PART_SIDE");
-        return e && *e == '1';
-    }();
-    return on;
-}
-static bool fixbig_side() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_FIXBIG_SIDE");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
 constexpr int32_t RETRY_GRID_MIN = 16;   // retry teams at least (history-sized grids)
-static bool retry_feedback() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_RETRY_FEEDBACK");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
-static bool sym_feedback() {
-    static const bool on = [] {
-        const char *e = getenv("IAS_SYM_FEEDBACK");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
 // IAS_SYM_BIG: 0 = rows beyond SYM2_MAX take the hash partitions / column
 // bitmap (A/B), 1 (default) = the sym5<32768> bins when B is too wide for the
 // column bitmap, 2 = also when it is not
@@ -2235,7 +2199,7 @@ static constexpr bool val_bins_covered() {
 static_assert(val_bins_covered(), "value-bin emission does not cover a bin's table");
 
 // Symbolic LDS bins in use: when the column-bitmap symbolic applies, those
-// up to SYM2_MAX (or below IAS_SYM_CBM_MIN products): the longer rows join
+// up to SYM2_MAX: the longer rows join
 // the partitioned bin (k_sym_cbm); otherwise also the two bins to 32,768
 // products (sym5<32768>; K4: 4.6 vs 31.5 ps per product in the hash
 // partitions), the longer rows hash-partitioned.
@@ -2245,15 +2209,7 @@ static_assert(val_bins_covered(), "value-bin emission does not cover a bin's tab
 // symbolic 115.5 ms at one workgroup per CU against 53.0 ms through the hash
 // partitions; round 6, profiles/r06/gtab/)
 static int sym_nval(bool cbm, bool wide = false) {
-    static const int nv = [] {
-        const char *e = getenv("IAS_SYM_CBM_MIN");
-        if (!e || !*e) return N_SYM2_LDS;
-        const long v = atol(e);
-        int n = 0;
-        while (n < N_SYM2_LDS && SYM2_BINS[n].upper < v) ++n;
-        return n;
-    }();
-    return cbm ? (big_mode() == 2 ? N_SYM2 : nv) : (big_mode() && !wide ? N_SYM2 : N_SYM2_LDS);
+    return cbm ? (big_mode() == 2 ? N_SYM2 : N_SYM2_LDS) : (big_mode() && !wide ? N_SYM2 : N_SYM2_LDS);
 }
 
 static BinSpec sym_spec(int nval = N_SYM2) {
@@ -2857,12 +2813,11 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
     // the other bins).
     // From the second call of a plan on, each bin's weight is its measured
     // duration beside the others per estimated product (the serial weights
-    // left the two queues 0.55 ms apart on K3'); IAS_SYM_FEEDBACK=0: serial
-    // weights only.
+    // left the two queues 0.55 ms apart on K3').
     int sym_lane[MAX_BINS] = {};
     double *sym_est = sym_est_prev;   // read back with the bins' durations by the next call
     std::fill(sym_est, sym_est + MAX_BINS, 0.0);
-    const bool fb = !serial && !small && sym_feedback();
+    const bool fb = !serial && !small;
     if (fb && !bin_ev[0])
         for (auto &e : bin_ev) HIPC(hipEventCreate(&e));
     {
@@ -2873,12 +2828,8 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         // beyond residency) run on the plan stream: on a side stream their
         // dispatch held its hardware queue, and the bins of the stream sharing
         // that queue waited behind it (K3: 3.2 ms of one queue idle at the
-        // end of the symbolic phase); IAS_PART_SIDE=1: a side stream (A/B)
-        if (c1.count[sym_part] > 0) {
-            sym_est[sym_part] = (double)c1.part_prod;
-            if (part_side())
-                jobs.push_back({weight(sym_part, cbm ? CBM_COST : 40.0) * sym_est[sym_part], sym_part});
-        }
+        // end of the symbolic phase; round 5)
+        if (c1.count[sym_part] > 0) sym_est[sym_part] = (double)c1.part_prod;
         for (int b = 1; b <= ss.nval; ++b)
             if (c1.count[b] > 0) {
                 const int32_t u = SYM2_BINS[b - 1].upper, l = b > 1 ? SYM2_BINS[b - 2].upper : 0;
@@ -2899,7 +2850,7 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         bin_rec[b] = true;
     };
     if ((c = c1.count[sym_part]) > 0) {
-        hipStream_t t = part_side() ? (hipStream_t)side_stream(sym_lane[sym_part]) : s;
+        hipStream_t t = s;
         bin_mark(sym_part, t, 0);
         if (cbm) {
             static bool cbm_done = false;
@@ -2983,14 +2934,13 @@ ias_status ias_plan::symbolic(const Rows &A, const Rows &B, int64_t rows, int64_
         // bin hands back few rows, and a full grid of LDS-heavy workgroups
         // waits for whole CUs beside the other bins (K3': 50 - 260 us per
         // retry launch for ~no rows) — so twice the rows this bin handed back
-        // on the plan's last call, when known (IAS_RETRY_FEEDBACK=0: the bin's
-        // rows)
+        // on the plan's last call, when known
         // (history only from a call that launched this bin — retry_prev is
         // -1 otherwise; at least RETRY_GRID_MIN teams, so an input that
         // crowds a bin the last call found clean still spreads its retries)
         retry_upper_cur[b & 15] = u;
         Sym2Args r2 = a2;
-        if (retry_feedback() && retry_prev[b & 15] >= 0 && retry_upper[b & 15] == u)
+        if (retry_prev[b & 15] >= 0 && retry_upper[b & 15] == u)
             r2.count = std::min<int32_t>(c, std::max<int32_t>(2 * retry_prev[b & 15] + 2, RETRY_GRID_MIN));
         if (u > SYM5_MAX) {   // SYM_CFG_BIG: sym5<32768>, its retries through the global tables
             const bool all = gtab_all(c1.wide_b);
@@ -3168,7 +3118,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     // the streaming pass — the phase's critical path — is launched first: the
     // host issues ~30 API calls for the others (~60 us on K3')
     IAS_TRY(fork());
-    int lane_no = (num_count[part_bin] > 0 && part_side() ? 1 : 0) + (num_count[wide_bin] > 0 ? 1 : 0);
+    int lane_no = num_count[wide_bin] > 0 ? 1 : 0;
     for (int i = 0; i < N_DW; ++i) lane_no += num_count[ns.nval + 3 + i] > 0 ? 1 : 0;
     auto launch_tables = [&]() -> ias_status {
         int tl = 0;
@@ -3176,9 +3126,9 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
         // beyond residency) on the plan stream: on a side stream their
         // dispatch held the hardware queue, and the fix-ups and short rows of
         // the stream sharing it waited behind (K3: 3.9 ms of fix-ups after
-        // the last streaming launch); IAS_PART_SIDE=1: a side stream (A/B)
+        // the last streaming launch; round 5)
         if (num_count[part_bin] > 0) {
-            hipStream_t t = part_side() ? (hipStream_t)side_stream(tl++) : s;
+            hipStream_t t = s;
             k_numeric_part<1024, 4, 14, 256><<<(unsigned)num_items, 1024, 0, t>>>(
                 ax, B, as<PartItem>(bufs[B_NITEM]), bm, out, &dc2->overflow);
             CHECK_LAUNCH("k_numeric_part", t);
@@ -3280,7 +3230,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
                         n2_mask |= 1 << k;
                     }
                     if (fix_split && k < 2) HIPC(hipEventRecord(fix_ev[k], t));
-                    if (fix_split && k == 0 && !fixbig_side()) IAS_TRY(launch_fix(t, 0));
+
                 }
                 fix_lane = lane_no;   // the fix-ups: the stream after this one
             }
@@ -3309,7 +3259,7 @@ ias_status ias_plan::numeric(const Rows &A, const Rows &B, const Out &out_in, ia
     if (fix_split) {
         hipStream_t f = (hipStream_t)side_stream(fix_lane);
         HIPC(hipStreamWaitEvent(f, fix_ev[0], 0));
-        if (fixbig_side()) IAS_TRY(launch_fix(f, 0));
+        IAS_TRY(launch_fix(f, 0));
         IAS_TRY(launch_fix(f, 1));
         HIPC(hipStreamWaitEvent(f, fix_ev[1], 0));
         IAS_TRY(launch_fix(f, 2));
