@@ -31,7 +31,7 @@ else
   timeout -k 10 600 $B --config k3 --no-host-e2e --cpu-full > $OUT/bench_k3.json 2> $OUT/bench_k3.err || exit $?
   timeout -k 10 300 $B --config k2 --no-host-e2e > $OUT/bench_k2.json 2> $OUT/bench_k2.err || exit $?
   timeout -k 10 300 $B --config k1 --no-host-e2e > $OUT/bench_k1.json 2> $OUT/bench_k1.err || exit $?
-  timeout -k 10 300 $B --config k1 --format dia --steps 20 --warmup 5 > $OUT/bench_k1_dia.json 2> $OUT/bench_k1_dia.err || exit $?
+  timeout -k 10 300 $B --config k1 --format dia --steps 200 --warmup 20 > $OUT/bench_k1_dia.json 2> $OUT/bench_k1_dia.err || exit $?
   timeout -k 10 300 $B --config k1w --format dia --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_k1w_dia.json 2> $OUT/bench_k1w_dia.err || exit $?
   timeout -k 10 300 $B --order sorted --steps 10 --warmup 2 --no-cpu-baseline --no-host-e2e --no-one-shot > $OUT/bench_k3p_sorted.json 2> $OUT/bench_k3p_sorted.err || exit $?
   timeout -k 10 900 $B --config k4 --steps 3 --warmup 1 --no-cpu-baseline --no-host-e2e --no-one-shot > $OUT/bench_k4_1gpu.json 2> $OUT/bench_k4_1gpu.err || exit $?
