@@ -16,7 +16,10 @@ SURVEY.md §8).  N>1: the K4 family, 2^(20+log2 N) rows, edge factor 24,
 seed 3 — N=8 is BASELINE's K4 (8M x 8M, avg 24 nnz/row).  Rows are sharded by
 estimated device cost (ias_partition_rows) across ranks with B replicated
 (broadcast once over RCCL before timing); per-rank work grows with the
-matrix, hence "scaling": "weak".  No collective inside the timed region (C
+matrix, hence "scaling": "weak".  The line names its series
+(config.family / config.series, series()); the N=1 line also times the K4
+family's own N=1 point (R-MAT 2^20, ef 24, seed 3) as `weak_anchor`, after
+its own loop.  A named --config is the same matrix for every N: "strong".  No collective inside the timed region (C
 stays sharded).  For N>1 the exchange step is measured after the timed loop
 (`allgatherv` in the line): one step compute-only and one step
 compute + the RCCL allgatherv that concatenates C on every rank
