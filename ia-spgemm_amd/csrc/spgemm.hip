@@ -1201,14 +1201,14 @@ __global__ __launch_bounds__(TEAM) void k_numeric_part(AxView ax, Rows B, const 
                                            bm.pref + bm.off[row], seg, scratch, out, overflow);
 }
 
-// Duplicate fix-up of the streaming rows that have duplicates: one wave per row.
+// Duplicate fix-up of streaming rows with 17 - 256 duplicates: one wave per row,
+// the list sorted in LDS (numeric_fixup_lds; the head scan it replaced was O(n^2)).
 constexpr int FIX_TPW = 4;
 __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int32_t count, Bitmap bm,
                                                         const int64_t *dup_off, const int32_t *dupn,
                                                         const int32_t *gdupt, const double *gdupval,
                                                         Out out) {
-    __shared__ int32_t dupt[FIX_TPW][256];
-    __shared__ double dval[FIX_TPW][256];
+    __shared__ unsigned long long key[FIX_TPW][2 * 256 + 256 / 64];
     const int team = threadIdx.x / WAVE;
     const int64_t idx = (int64_t)blockIdx.x * FIX_TPW + team;
     if (idx >= count) return;
@@ -1216,8 +1216,8 @@ __global__ __launch_bounds__(WAVE *FIX_TPW) void k_fixup(const RowRef *list, int
     const int32_t nd = dupn[row];
     if (nd <= 0 || nd > 256) return;
     const int64_t off = bm.off[row];
-    numeric_fixup_row<WAVE>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
-                            gdupval + dup_off[row], nd, dupt[team], dval[team], out);
+    numeric_fixup_lds<WAVE, 256>(row, bm.bits + off, bm.pref + off, gdupt + dup_off[row],
+                                 gdupval + dup_off[row], nd, key[team], out);
 }
 
 // Duplicate fix-up of streaming rows with short lists (<= 16): one lane per

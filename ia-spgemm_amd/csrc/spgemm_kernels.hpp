@@ -721,35 +721,40 @@ __device__ __forceinline__ int32_t symbolic_bucket_row(const uint2 *bk, int32_t 
 // product is parked at dupval[dup_off[row] + d] (d = duplicates before it in
 // the row) for the fix-up kernels below.
 
-// Fix-up of one streaming row with duplicates: each column's duplicate
-// products are added to its entry in product order (one lane per column).
-// The list and its values are staged in LDS first: the per-column walks then
-// read LDS, not one dependent global load per duplicate.
-template <int TEAM>
-__device__ __forceinline__ void numeric_fixup_row(int64_t row, const uint32_t *bits, const uint32_t *bpref,
-                                                  const int32_t *gdupt, const double *gdupval,
-                                                  int32_t ndup, int32_t *dupt, double *dval, const Out &out) {
+// Bitonic sort (ascending) of key[0, n2), n2 a power of two <= CAP, by a team
+// of TEAM lanes.  Each stage's compare-exchange pairs are numbered q = 0 ..
+// n2/2 - 1 (lower index: q with a zero bit inserted at the stride's
+// position), so every lane is busy, and a lane's PP pairs are all read before
+// any is compared: one LDS round trip per stage rather than one per pair (the
+// per-pair form waits on each read, ~60 us per 4096-key list).
+template <int TEAM, int CAP, typename K>
+__device__ __forceinline__ void bitonic_lds(K *key, uint32_t n2) {
     using TM = Team<TEAM>;
-    const int lane = TM::lane();
-    for (int32_t i = lane; i < ndup; i += TEAM) {
-        dupt[i] = gdupt[i];
-        dval[i] = gdupval[i];
-    }
-    TM::sync();
-    const int64_t st = out.start(row);
-    const uint32_t nnz = (uint32_t)out.len[row];
-    for (int32_t i = lane; i < ndup; i += TEAM) {
-        const int32_t t = dupt[i];
-        bool head = true;
-        for (int32_t j = 0; j < i && head; ++j) head = dupt[j] != t;
-        if (!head) continue;
-        const uint32_t p = (uint32_t)t;
-        const uint32_t rk = bpref[p >> 5] + (uint32_t)__popc(bits[p >> 5] & ((1u << (p & 31)) - 1u));
-        const int64_t pos = st + (out.order == 0 ? (int64_t)(nnz - 1u - rk) : (int64_t)rk);
-        double v = out.val[pos];
-        for (int32_t j = i; j < ndup; ++j)
-            if (dupt[j] == t) v = v + dval[j];
-        out.val[pos] = v;
+    constexpr int PP = (CAP / 2 + TEAM - 1) / TEAM;
+    const uint32_t lane = (uint32_t)TM::lane(), np = n2 >> 1;
+    for (uint32_t k = 2; k <= n2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            K a[PP], b[PP];
+            uint32_t lo[PP];
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                const uint32_t q = (uint32_t)r * TEAM + lane;
+                lo[r] = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                if (q < np) {
+                    a[r] = key[lo[r]];
+                    b[r] = key[lo[r] | j];
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < PP; ++r) {
+                const uint32_t q = (uint32_t)r * TEAM + lane;
+                if (q < np && (a[r] > b[r]) == ((lo[r] & k) == 0)) {
+                    key[lo[r]] = b[r];
+                    key[lo[r] | j] = a[r];
+                }
+            }
+            TM::sync();
+        }
     }
 }
 
@@ -774,21 +779,7 @@ __device__ __forceinline__ void numeric_fixup_big(int64_t row, const uint32_t *b
     for (uint32_t i = lane; i < n2; i += TEAM)
         key[i] = i < (uint32_t)ndup ? (((unsigned long long)(uint32_t)gdupt[i] << 32) | i) : ~0ull;
     TM::sync();
-    for (uint32_t k = 2; k <= n2; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = lane; i < n2; i += TEAM) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long a = key[i], b = key[ixj];
-                    if ((a > b) == ((i & k) == 0)) {
-                        key[i] = b;
-                        key[ixj] = a;
-                    }
-                }
-            }
-            TM::sync();
-        }
-    }
+    bitonic_lds<TEAM, CAP>(key, n2);
     uint32_t tt[PER];
     double vv[PER];
     bool hd[PER];
@@ -842,21 +833,7 @@ __device__ __forceinline__ void numeric_fixup_lds(int64_t row, const uint32_t *b
     for (uint32_t i = lane; i < n2; i += TEAM)
         key[i] = i < (uint32_t)ndup ? (((unsigned long long)(uint32_t)gdupt[i] << 32) | i) : ~0ull;
     TM::sync();
-    for (uint32_t k = 2; k <= n2; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = lane; i < n2; i += TEAM) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long a = key[i], b = key[ixj];
-                    if ((a > b) == ((i & k) == 0)) {
-                        key[i] = b;
-                        key[ixj] = a;
-                    }
-                }
-            }
-            TM::sync();
-        }
-    }
+    bitonic_lds<TEAM, CAP>(key, n2);
     // run heads and the values in sorted order (the loads of a group of
     // entries issued together)
     constexpr int G = 4;
