@@ -1538,32 +1538,18 @@ __device__ __forceinline__ void bitonic(int32_t *sk, double *sv, uint32_t cap) {
     }
 }
 
-// keys only (distinct int32), ascending
-template <int TEAM>
-__device__ __forceinline__ void bitonic_keys(int32_t *sk, uint32_t cap) {
-    const int lane = Team<TEAM>::lane();
-    for (uint32_t k = 2; k <= cap; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = lane; i < cap; i += TEAM) {
-                const uint32_t ixj = i ^ j;
-                if (ixj > i) {
-                    const bool up = (i & k) == 0;
-                    const int32_t a = sk[i], b = sk[ixj];
-                    if ((a > b) == up) {
-                        sk[i] = b;
-                        sk[ixj] = a;
-                    }
-                }
-            }
-            Team<TEAM>::sync();
-        }
-    }
-}
-// a bucket of more keys than this sends the row to bitonic_keys: its m^2 / TEAM
+// a bucket of more keys than this sends the row to the bitonic sort: its m^2 / TEAM
 // rank loop then costs about what the bitonic sort does (32 = 8x the mean of
 // 4 sent most of K3's R-MAT rows there: sorted K3' 19.5 -> 41.7 ms)
 constexpr uint32_t SORTB_HEAVY = 256;
 
+// A listed row's extent from its list entry (the sort binning stores the
+// row's start relative to ptr[0] and its length): no dependent row-pointer
+// load after the list entry's.
+__device__ __forceinline__ void sort_ref_span(const RowRef &ref, const int64_t *ptr, int64_t &o, int32_t &n) {
+    o = ref.q0 + (ptr ? ptr[0] : 0);
+    n = ref.n;
+}
 __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t *len, int64_t stride,
                                               int64_t row, int64_t &o, int32_t &n) {
     if (ptr) {
@@ -1575,54 +1561,88 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
     }
 }
 
+// A team barrier for LDS only: waits for this wave's LDS operations, not for
+// its global loads in flight (a workgroup fence waits for both, which would
+// stall the sort's prefetch at the next barrier).  The "memory" clobber keeps
+// the compiler from moving memory operations across it.
+template <bool MULTI>
+__device__ __forceinline__ void lds_sync() {
+    if constexpr (MULTI) {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 // Rows of up to TEAM * E entries sorted by a bucket pass in LDS: the row's
 // columns are distinct, so an entry's sorted position is the number of the
-// row's columns below it.  Buckets split the row's column range [min, max]
-// into nb ~ n/4 equal parts (a monotone map, so bucket order is key order);
-// an entry's position = its bucket's start (a scan of the bucket counts) +
-// the keys of its bucket below it (a short loop over the bucket's keys,
-// which are ~4 on average: O(n) work per row, values never leave registers).
-// One read and one write of each entry, three or four team barriers per row
-// (the bitonic sort it replaces needed one per stage, log2(n)^2 / 2 of them).
+// row's columns below it.  Buckets split the row's columns into nb ~ n/2 ..
+// n/4 parts by a monotone map (bucket order is key order); an entry's
+// position = its bucket's start (a scan of the bucket counts) + the keys of
+// its bucket below it (values never leave registers).
+//   * The map is equalised: R-MAT rows crowd their low columns (~n^0.74 of a
+//     row's keys below column x^0.74), so equal-width buckets held 10 - 14
+//     keys per key on average and a wave waited on its fullest lane.  A
+//     coarse histogram (G equal-width bins) and its scan give each coarse bin
+//     fine buckets in proportion to its keys: 6 - 7 keys per key.
+//   * A lane's E bucket walks go in lockstep, the E reads of a step issued
+//     together: one LDS round trip per step of the longest walk, not one per
+//     key of every walk (modelled on K3''s rows: 217 -> 16 round trips per
+//     wave on the 4,097 - 8,192-entry rows).
+// Every team stages the sorted row in LDS and writes it out contiguously (the
+// 1,024-lane teams in two halves of values, 72 KB: their scattered stores
+// touched a cache line per lane).
 template <int TEAM, int E, int TPW>
 __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, int32_t count,
-                                                           const int64_t *ptr, const int32_t *len,
-                                                           int64_t stride, int32_t *col, double *val) {
+                                                           const int64_t *ptr, int32_t *col, double *val) {
     static_assert(TEAM <= 64 || TPW == 1, "multi-wave teams own their workgroup");
     using TM = Team<TEAM>;
     constexpr int CAP = TEAM * E;
-    constexpr int NBM = CAP / 4 > 0 ? CAP / 4 : 1;   // most buckets
-    constexpr int NBT = (NBM + TEAM - 1) / TEAM;      // bucket counts per thread in the scan
-    // the sorted row staged in LDS and written out contiguously, except for
-    // the 1024-lane teams (the staging's 64 KB leave one team per CU: 2.03 vs
-    // 1.79 ms on K3''s 4,097 - 8,192-entry rows)
-    constexpr bool STAGE = TEAM < 1024;
+    constexpr int NBM = TEAM < 1024 ? CAP : CAP / 2;        // most buckets
+    constexpr int NBT = (NBM + TEAM - 1) / TEAM;            // bucket counts per thread in the scan
+    constexpr int G = CAP / 2 < 2 ? 1 : (CAP / 2 < 256 ? CAP / 2 : 256);   // coarse bins
+    constexpr int GT = (G + TEAM - 1) / TEAM;
+    constexpr int SVC = TEAM < 1024 ? CAP : CAP / 2;        // values staged per round
+    static_assert(2 * SVC >= NBM + G + 2, "the bucket counts and the coarse bins overlay the value staging");
     __shared__ int32_t sk[TPW][CAP];
-    __shared__ double sv[TPW][STAGE ? CAP : 1];
-    __shared__ uint32_t hist[TPW][NBM + 1];
+    __shared__ double sv[TPW][SVC];
     __shared__ int scratch[TPW][64];
     const int team = (TPW == 1) ? 0 : (int)(threadIdx.x / TEAM);
+    // the bucket counts / starts and the coarse bins live in the value
+    // staging area, which is dead until the ranks are known
+    uint32_t *const hist = (uint32_t *)sv[team];
+    uint32_t *const gh = hist + NBM + 1;
     const int lane = TM::lane();
-    const int64_t idx = (int64_t)blockIdx.x * TPW + team;
-    const int64_t row = idx < count ? list[idx].row : -1;
+    // persistent teams: row i + 1's list entry is loaded at the top of row
+    // i and its columns (with row i's values) once row i's buckets are
+    // counted, so they arrive while row i is ranked and written (the load
+    // chain was ~6 of a row's 13 - 20 us)
+    const int64_t rstride = (int64_t)gridDim.x * TPW;
+    int64_t idx = (int64_t)blockIdx.x * TPW + team;
+    Timer tm;   // timing builds only (phases: 0 loads + range, 1 coarse bins, 2 fine buckets, 3 bucket scan,
+                // 4 ranks, 5 staging, 6 stores issued)
+    tm.start();
+    RowRef ref = idx < count ? list[idx] : RowRef{0, -1, 0};
     int64_t o = 0;
     int32_t n = 0;
-    if (row >= 0) sort_row_span(ptr, len, stride, row, o, n);
+    if (ref.row >= 0) sort_ref_span(ref, ptr, o, n);
     int32_t c[E];
-    double v[E];
-    int32_t lo = INT32_MAX, hi = INT32_MIN;
 #pragma unroll
     for (int k = 0; k < E; ++k) {
         const int e = k * TEAM + lane;
-        c[k] = 0;
-        v[k] = 0.0;
-        if (e < n) {
-            c[k] = col[o + e];
-            v[k] = val[o + e];
+        c[k] = e < n ? col[o + e] : 0;
+    }
+    while (ref.row >= 0) {   // uniform over the team
+    const RowRef nref = idx + rstride < count ? list[idx + rstride] : RowRef{0, -1, 0};
+    int32_t lo = INT32_MAX, hi = INT32_MIN;
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) {
             lo = min(lo, c[k]);
             hi = max(hi, c[k]);
         }
-    }
     // the row's column range (team min / max)
     {
         constexpr int W = TEAM < WAVE ? TEAM : WAVE;
@@ -1645,26 +1665,69 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
             }
         }
     }
-    // nb: a power of two near n / 4 (at least 1, at most NBM)
+    tm.mark(0);
+    // nb: a power of two in (n / 2, n] (at least 1, at most NBM): ~1.5 keys
+    // per bucket (K3''s rows, equalised: 5 - 11 lockstep steps per wave)
     int nb = 1;
-    while (nb < NBM && 4 * nb * 2 <= n) nb <<= 1;
-    for (int i = lane; i <= nb; i += TEAM) hist[team][i] = 0u;
+    while (nb < NBM && 2 * nb <= n) nb <<= 1;
+    // coarse bins of 2^sh columns, fewer than G of them over [lo, hi]
+    const uint32_t range = n > 0 ? (uint32_t)(hi - lo) : 0u;
+    int sh = 0;
+    while ((range >> sh) >= (uint32_t)G) ++sh;
+    for (int i = lane; i <= nb; i += TEAM) hist[i] = 0u;
+    for (int i = lane; i <= G; i += TEAM) gh[i] = 0u;
     TM::sync();   // (multi-wave: also every wave's min / max read before scratch is reused)
-    const float scale = n > 0 ? (float)nb / ((float)((uint32_t)(hi - lo)) + 1.0f) : 0.0f;
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) atomicAdd(&gh[(uint32_t)(c[k] - lo) >> sh], 1u);
+    TM::sync();
+    {
+        uint32_t cnt[GT], sum = 0;
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            const int i = lane * GT + j;
+            cnt[j] = i < G ? gh[i] : 0u;
+            sum += cnt[j];
+        }
+        int tot;
+        uint32_t run = (uint32_t)TM::excl_sum((int)sum, tot, scratch[team]);
+        TM::sync();   // every count read before the starts overwrite them
+#pragma unroll
+        for (int j = 0; j < GT; ++j) {
+            const int i = lane * GT + j;
+            if (i < G) gh[i] = run;
+            run += cnt[j];
+        }
+        if (lane == 0) gh[G] = (uint32_t)n;
+    }
+    TM::sync();
+    tm.mark(1);
+    // fine bucket: nb / n * (keys of the coarse bins below + the key's share
+    // of its own bin's keys) — non-decreasing in the column (float products
+    // and sums of non-negative terms round monotonically; a bin's share stays
+    // at most its count, where the next bin starts)
+    const float fnb = n > 0 ? (float)nb / (float)n : 0.0f;
+    const float winv = 1.0f / (float)(1u << sh);
     int b[E];
     uint32_t pib[E];
 #pragma unroll
     for (int k = 0; k < E; ++k) {
         const int e = k * TEAM + lane;
-        b[k] = min((int)((float)((uint32_t)(c[k] - lo)) * scale), nb - 1);
+        b[k] = 0;
         pib[k] = 0u;
-        if (e < n) pib[k] = atomicAdd(&hist[team][b[k]], 1u);
+        if (e < n) {
+            const uint32_t d = (uint32_t)(c[k] - lo), g = d >> sh;
+            const uint32_t g0 = gh[g], g1 = gh[g + 1];
+            const float t = (float)g0 + (float)(d & ((1u << sh) - 1u)) * ((float)(g1 - g0) * winv);
+            b[k] = min((int)(t * fnb), nb - 1);
+            pib[k] = atomicAdd(&hist[b[k]], 1u);
+        }
     }
     TM::sync();
+    tm.mark(2);
     // bucket starts: exclusive scan of the counts (NBT per thread, in order);
     // bits 16+ of the scanned value count the lanes holding a bucket of more
-    // than SORTB_HEAVY keys (clustered columns with a far outlier put most of
-    // the row into a few buckets, and the in-bucket rank loop is quadratic)
+    // than SORTB_HEAVY keys (the in-bucket rank walk is quadratic)
     bool heavy;
     {
         uint32_t cnt[NBT], sum = 0;
@@ -1672,7 +1735,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            cnt[j] = i < nb ? hist[team][i] : 0u;
+            cnt[j] = i < nb ? hist[i] : 0u;
             sum += cnt[j];
             big = big || cnt[j] > SORTB_HEAVY;
         }
@@ -1683,26 +1746,52 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
 #pragma unroll
         for (int j = 0; j < NBT; ++j) {
             const int i = lane * NBT + j;
-            if (i < nb) hist[team][i] = run;
+            if (i < nb) hist[i] = run;
             run += cnt[j];
         }
-        if (lane == 0) hist[team][nb] = (uint32_t)n;
+        if (lane == 0) hist[nb] = (uint32_t)n;
     }
     TM::sync();
+    tm.mark(3);
+    // this row's values and the next row's columns, in flight from here
+    // (the values are first needed by the staging)
+    int64_t no = 0;
+    int32_t nn = 0;
+    if (nref.row >= 0) sort_ref_span(nref, ptr, no, nn);
+    double v[E];
+    int32_t cn[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k) {
+        const int e = k * TEAM + lane;
+        v[k] = e < n ? val[o + e] : 0.0;
+        cn[k] = e < nn ? col[no + e] : 0;
+    }
     uint32_t r[E];
     if (!heavy) {
 #pragma unroll
         for (int k = 0; k < E; ++k)
-            if (k * TEAM + lane < n) sk[team][hist[team][b[k]] + pib[k]] = c[k];
-        TM::sync();
+            if (k * TEAM + lane < n) sk[team][hist[b[k]] + pib[k]] = c[k];
+        lds_sync<TM::MULTI>();
+        uint32_t s0[E], sz[E], mx = 0u;
 #pragma unroll
         for (int k = 0; k < E; ++k) {
-            r[k] = 0u;
-            if (k * TEAM + lane >= n) continue;
-            const uint32_t s0 = hist[team][b[k]], s1 = hist[team][b[k] + 1];
-            uint32_t x = s0;
-            for (uint32_t j = s0; j < s1; ++j) x += sk[team][j] < c[k] ? 1u : 0u;
-            r[k] = x;
+            s0[k] = 0u;
+            sz[k] = 0u;
+            if (k * TEAM + lane < n) {
+                s0[k] = hist[b[k]];
+                sz[k] = hist[b[k] + 1] - s0[k];
+            }
+            r[k] = s0[k];
+            mx = max(mx, sz[k]);
+        }
+        // branch-free steps (a clamped read for a finished walk): the E reads
+        // of a step are issued before any compare
+        for (uint32_t j = 0; j < mx; ++j) {
+            int32_t kj[E];
+#pragma unroll
+            for (int k = 0; k < E; ++k) kj[k] = sk[team][sz[k] ? s0[k] + min(j, sz[k] - 1u) : 0u];
+#pragma unroll
+            for (int k = 0; k < E; ++k) r[k] += (j < sz[k] && kj[k] < c[k]) ? 1u : 0u;
         }
     } else {
         // skewed buckets: the keys alone sorted in LDS (bitonic, padded to a
@@ -1715,8 +1804,8 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
             const int e = k * TEAM + lane;
             if ((uint32_t)e < cap) sk[team][e] = e < n ? c[k] : INT32_MAX;
         }
-        TM::sync();
-        bitonic_keys<TEAM>(sk[team], cap);
+        lds_sync<TM::MULTI>();
+        bitonic_lds<TEAM, CAP>(sk[team], cap);
 #pragma unroll
         for (int k = 0; k < E; ++k) {
             r[k] = 0u;
@@ -1730,31 +1819,43 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
             r[k] = lo2;
         }
     }
-    if constexpr (!STAGE) {
+    // the entries land at their ranks in LDS, then leave in order (a lane's
+    // scattered global store touched its own cache line)
+    lds_sync<TM::MULTI>();   // every rank read of sk done
+    tm.mark(4);
 #pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (k * TEAM + lane < n) {
-                col[o + r[k]] = c[k];
-                val[o + r[k]] = v[k];
-            }
-    } else {
-        // the entries land at their ranks in LDS, then leave in order: a
-        // lane's scattered global store touched its own cache line (one lane
-        // per cycle in the texture unit), these are contiguous (K3' sorted
-        // 22.0 -> 21.0 ms)
-        TM::sync();   // every rank read of sk done
+    for (int k = 0; k < E; ++k)
+        if (k * TEAM + lane < n) {
+            sk[team][r[k]] = c[k];
+            if (r[k] < (uint32_t)SVC) sv[team][r[k]] = v[k];
+        }
+    lds_sync<TM::MULTI>();
+    tm.mark(5);
+    for (int e = lane; e < n; e += TEAM) {
+        col[o + e] = sk[team][e];
+        if (e < SVC) val[o + e] = sv[team][e];
+    }
+    if constexpr (SVC < CAP) {
+        if (n > SVC) {   // uniform: one team per workgroup here
+            lds_sync<TM::MULTI>();
 #pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (k * TEAM + lane < n) {
-                sk[team][r[k]] = c[k];
-                sv[team][r[k]] = v[k];
-            }
-        TM::sync();
-        for (int e = lane; e < n; e += TEAM) {
-            col[o + e] = sk[team][e];
-            val[o + e] = sv[team][e];
+            for (int k = 0; k < E; ++k)
+                if (k * TEAM + lane < n && r[k] >= (uint32_t)SVC) sv[team][r[k] - SVC] = v[k];
+            lds_sync<TM::MULTI>();
+            for (int e = SVC + lane; e < n; e += TEAM) val[o + e] = sv[team][e - SVC];
         }
     }
+    lds_sync<TM::MULTI>();   // the staging read out before the next row's counts overwrite it
+    tm.mark(6);
+    tm.done();
+#pragma unroll
+    for (int k = 0; k < E; ++k) c[k] = cn[k];
+    ref = nref;
+    o = no;
+    n = nn;
+    idx += rstride;
+    }
+    tm.flush(TEAM == 64 ? (E == 8 ? 12 : 11) : 6 + ilog2(TEAM), lane == 0 && team == 0);   // slots 11 - 16
 }
 
 __global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_t count,
@@ -1794,62 +1895,128 @@ __global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_
 // SORTBM_COLS (the bitmap: 128 KB of LDS + 16 KB of prefixes).
 constexpr int SORTBM_T = 1024;
 constexpr int32_t SORTBM_COLS = 1 << 20;
+static_assert(SORTBM_COLS / 256 <= SORTBM_T * 4, "bitmap_prefix8: at most four groups per thread");
 constexpr size_t sortbm_lds(int32_t cols) {
     return 4ull * (((size_t)cols + 255) / 256 * 8) + 4ull * (((size_t)cols + 255) / 256 + 1) + 4ull * 64;
 }
+// Sorted position of column c from the row's bitmap: the exclusive prefix of
+// its 8-word group plus the popcounts of the group's words below it, the
+// group read as two 16-byte loads (one LDS round trip; the word-by-word loop
+// it replaces waited on up to seven).
+__device__ __forceinline__ int bitmap_rank(const uint32_t *bits, const int32_t *pre8, uint32_t c) {
+    const uint32_t wi = c >> 5, g = wi >> 3, j = wi & 7u;
+    const uint4 a = ((const uint4 *)bits)[2 * g], b = ((const uint4 *)bits)[2 * g + 1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    int p = pre8[g];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t m = q < j ? ~0u : (q == j ? (1u << (c & 31)) - 1u : 0u);
+        p += __popc(w[q] & m);
+    }
+    return p;
+}
+
+// Exclusive popcount prefix of every 8-word group of the bitmap (pre8[g]):
+// whole groups per thread, each read as two 16-byte loads, the group sums
+// kept in registers for the second half (one pass over the bitmap, where a
+// word-by-word count pass and a prefix pass read it twice, one word per wait)
+constexpr int SORTBM_GPT = 4;   // groups per thread: 2^20 columns = 4,096 groups
+__device__ __forceinline__ void bitmap_prefix8(const uint32_t *bits, int32_t *pre8, int NW, int *scratch) {
+    const int tid = (int)threadIdx.x, ng = NW / 8;
+    const int gpt = (ng + SORTBM_T - 1) / SORTBM_T;
+    int gs[SORTBM_GPT], cnt = 0;
+#pragma unroll
+    for (int j = 0; j < SORTBM_GPT; ++j) {
+        const int g = tid * gpt + j;
+        gs[j] = 0;
+        if (j < gpt && g < ng) {
+            const uint4 a = ((const uint4 *)bits)[2 * g], b = ((const uint4 *)bits)[2 * g + 1];
+            gs[j] = __popc(a.x) + __popc(a.y) + __popc(a.z) + __popc(a.w) + __popc(b.x) + __popc(b.y) +
+                    __popc(b.z) + __popc(b.w);
+        }
+        cnt += gs[j];
+    }
+    int tot;
+    int run = Team<SORTBM_T>::excl_sum(cnt, tot, scratch);
+#pragma unroll
+    for (int j = 0; j < SORTBM_GPT; ++j) {
+        const int g = tid * gpt + j;
+        if (j < gpt && g < ng) pre8[g] = run;
+        run += gs[j];
+    }
+}
+
+// the long rows' passes take SORTBM_B entries per thread at a time, their
+// loads issued together (one global round trip per batch, not per entry)
+constexpr int SORTBM_B = 8;
 __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, int32_t count, const int64_t *ws_off,
                                                          const int64_t *ptr, const int32_t *len, int64_t stride,
                                                          int32_t *col, double *val, int32_t ncols, int32_t *wcol,
                                                          double *wval) {
-    extern __shared__ uint32_t sbm[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t sbm[];
     const int NW = (ncols + 255) / 256 * 8;   // bitmap words, a multiple of 8
     uint32_t *bits = sbm;
     int32_t *pre8 = (int32_t *)(bits + NW);    // exclusive popcount prefix per 8 words
     int *scratch = pre8 + NW / 8 + 1;
     const int tid = (int)threadIdx.x;
-    const int per = (NW + SORTBM_T - 1) / SORTBM_T;   // words per thread, a multiple of 8 when NW > T * 8
+    constexpr int BT = SORTBM_B * SORTBM_T;
     for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
         int64_t o;
         int32_t n;
-        sort_row_span(ptr, len, stride, list[idx].row, o, n);
+        sort_ref_span(list[idx], ptr, o, n);
         const int64_t w0 = ws_off[idx];
         for (int i = tid; i < NW / 4; i += SORTBM_T) ((uint4 *)bits)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
-        for (int32_t e = tid; e < n; e += SORTBM_T) {
-            const uint32_t c = (uint32_t)col[o + e];
-            atomicOr(&bits[c >> 5], 1u << (c & 31));
-        }
-        __syncthreads();
-        // thread t: words [t * per, (t + 1) * per)
-        int cnt = 0;
-        for (int j = 0; j < per; ++j) {
-            const int wi = tid * per + j;
-            cnt += wi < NW ? __popc(bits[wi]) : 0;
-        }
-        int tot;
-        int run = Team<SORTBM_T>::excl_sum(cnt, tot, scratch);
-        for (int j = 0; j < per; ++j) {
-            const int wi = tid * per + j;
-            if (wi < NW) {
-                if ((wi & 7) == 0) pre8[wi >> 3] = run;
-                run += __popc(bits[wi]);
+        for (int32_t e0 = 0; e0 < n; e0 += BT) {
+            uint32_t c[SORTBM_B];
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k) {
+                const int32_t e = e0 + k * SORTBM_T + tid;
+                c[k] = e < n ? (uint32_t)col[o + e] : 0u;
             }
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k)
+                if (e0 + k * SORTBM_T + tid < n) atomicOr(&bits[c[k] >> 5], 1u << (c[k] & 31));
         }
         __syncthreads();
-        for (int32_t e = tid; e < n; e += SORTBM_T) {
-            const uint32_t c = (uint32_t)col[o + e];
-            const double v = val[o + e];
-            const uint32_t wi = c >> 5;
-            int pos = pre8[wi >> 3] + __popc(bits[wi] & ((1u << (c & 31)) - 1u));
-            for (uint32_t k = wi & ~7u; k < wi; ++k) pos += __popc(bits[k]);
-            wcol[w0 + pos] = (int32_t)c;
-            wval[w0 + pos] = v;
+        bitmap_prefix8(bits, pre8, NW, scratch);
+        __syncthreads();
+        for (int32_t e0 = 0; e0 < n; e0 += BT) {
+            uint32_t c[SORTBM_B];
+            double v[SORTBM_B];
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k) {
+                const int32_t e = e0 + k * SORTBM_T + tid;
+                c[k] = e < n ? (uint32_t)col[o + e] : 0u;
+                v[k] = e < n ? val[o + e] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k)
+                if (e0 + k * SORTBM_T + tid < n) {
+                    const int pos = bitmap_rank(bits, pre8, c[k]);
+                    wcol[w0 + pos] = (int32_t)c[k];
+                    wval[w0 + pos] = v[k];
+                }
         }
         __threadfence_block();
         __syncthreads();
-        for (int32_t e = tid; e < n; e += SORTBM_T) {
-            col[o + e] = wcol[w0 + e];
-            val[o + e] = wval[w0 + e];
+        for (int32_t e0 = 0; e0 < n; e0 += BT) {
+            int32_t c[SORTBM_B];
+            double v[SORTBM_B];
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k) {
+                const int32_t e = e0 + k * SORTBM_T + tid;
+                c[k] = e < n ? wcol[w0 + e] : 0;
+                v[k] = e < n ? wval[w0 + e] : 0.0;
+            }
+#pragma unroll
+            for (int k = 0; k < SORTBM_B; ++k) {
+                const int32_t e = e0 + k * SORTBM_T + tid;
+                if (e < n) {
+                    col[o + e] = c[k];
+                    val[o + e] = v[k];
+                }
+            }
         }
         __syncthreads();
     }
@@ -1869,7 +2036,7 @@ constexpr size_t sortb2_lds(int32_t cols) {
 __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap16(const RowRef *list, int32_t count, const int64_t *ptr,
                                                            const int32_t *len, int64_t stride, int32_t *col,
                                                            double *val, int32_t ncols) {
-    extern __shared__ uint32_t sbm[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t sbm[];
     const int NW = (ncols + 255) / 256 * 8;   // bitmap words, a multiple of 8
     const size_t area = sortb2_lds(ncols) - 4ull * (NW / 8 + 1) - 4ull * 64;   // bitmap / staging bytes
     uint32_t *bits = sbm;
@@ -1878,11 +2045,12 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap16(const RowRef *list, 
     int32_t *pre8 = (int32_t *)((char *)sbm + area);
     int *scratch = pre8 + NW / 8 + 1;
     const int tid = (int)threadIdx.x;
-    const int per = (NW + SORTBM_T - 1) / SORTBM_T;
+    Timer tm;   // timing builds only (phases: 0 loads + clear, 1 bitmap, 2 prefix, 3 ranks, 4 staging + stores)
+    tm.start();
     for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
         int64_t o;
         int32_t n;
-        sort_row_span(ptr, len, stride, list[idx].row, o, n);
+        sort_ref_span(list[idx], ptr, o, n);
         int32_t *const rc = col + o;
         double *const rv = val + o;
         int32_t c[SORTB2_E];
@@ -1895,37 +2063,23 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap16(const RowRef *list, 
         }
         for (int i = tid; i < NW / 4; i += SORTBM_T) ((uint4 *)bits)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
+        tm.mark(0);
 #pragma unroll
         for (int k = 0; k < SORTB2_E; ++k)
             if (k * SORTBM_T + tid < n) atomicOr(&bits[(uint32_t)c[k] >> 5], 1u << (c[k] & 31));
         __syncthreads();
-        int cnt = 0;
-        for (int j = 0; j < per; ++j) {
-            const int wi = tid * per + j;
-            cnt += wi < NW ? __popc(bits[wi]) : 0;
-        }
-        int tot;
-        int run = Team<SORTBM_T>::excl_sum(cnt, tot, scratch);
-        for (int j = 0; j < per; ++j) {
-            const int wi = tid * per + j;
-            if (wi < NW) {
-                if ((wi & 7) == 0) pre8[wi >> 3] = run;
-                run += __popc(bits[wi]);
-            }
-        }
+        tm.mark(1);
+        bitmap_prefix8(bits, pre8, NW, scratch);
         __syncthreads();
+        tm.mark(2);
         int32_t pos[SORTB2_E];
 #pragma unroll
         for (int k = 0; k < SORTB2_E; ++k) {
             pos[k] = 0;
-            if (k * SORTBM_T + tid < n) {
-                const uint32_t cc = (uint32_t)c[k], wi = cc >> 5;
-                int p = pre8[wi >> 3] + __popc(bits[wi] & ((1u << (cc & 31)) - 1u));
-                for (uint32_t q = wi & ~7u; q < wi; ++q) p += __popc(bits[q]);
-                pos[k] = p;
-            }
+            if (k * SORTBM_T + tid < n) pos[k] = bitmap_rank(bits, pre8, (uint32_t)c[k]);
         }
         __syncthreads();   // every bitmap read done: the area becomes the staging row
+        tm.mark(3);
         for (int32_t lo = 0; lo < n; lo += SORTB2_CH) {
             const int32_t m = min(SORTB2_CH, n - lo);
 #pragma unroll
@@ -1941,7 +2095,10 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap16(const RowRef *list, 
             }
             __syncthreads();
         }
+        tm.mark(4);
+        tm.done();
     }
+    tm.flush(17, tid == 0);
 }
 
 __global__ __launch_bounds__(256) void k_wide_gather(const RowRef *list, int32_t count,
@@ -3317,6 +3474,15 @@ static void scan_i32(const int32_t *in, int64_t n, int64_t *part, int64_t *out, 
 }
 
 // ------------------------------------------------------------------ row sort host
+// A bucket-sort bin: persistent teams, one workgroup per resident slot at most.
+template <int TEAM, int E, int TPW>
+static void sort_bucket(const RowRef *list, int32_t c, const int64_t *ptr, int32_t *col, double *val,
+                        hipStream_t t) {
+    auto kern = k_sort_bucket<TEAM, E, TPW>;
+    const int64_t grid = std::min<int64_t>(grid_for(c, TPW), resident_blocks(kern, TEAM * TPW, 0));
+    kern<<<(unsigned)std::max<int64_t>(grid, 1), TEAM * TPW, 0, t>>>(list, c, ptr, col, val);
+}
+
 static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32_t *len_in,
                                  int64_t stride, int64_t rows, int32_t *col, double *val) {
     if (rows <= 0) return IAS_SUCCESS;
@@ -3406,20 +3572,13 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     auto launch = [&](int b, hipStream_t t) -> hipError_t {
         int c;
         switch (b) {
-        case 1: c = hc.count[1];
-            k_sort_bucket<64, 1, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(1), c, ptr, len, stride, col, val); break;
-        case 2: c = hc.count[2];
-            k_sort_bucket<64, 4, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(2), c, ptr, len, stride, col, val); break;
-        case 3: c = hc.count[3];
-            k_sort_bucket<64, 8, 4><<<grid_for(c, 4), 256, 0, t>>>(lst(3), c, ptr, len, stride, col, val); break;
-        case 4: c = hc.count[4];
-            k_sort_bucket<128, 8, 1><<<c, 128, 0, t>>>(lst(4), c, ptr, len, stride, col, val); break;
-        case 5: c = hc.count[5];
-            k_sort_bucket<256, 8, 1><<<c, 256, 0, t>>>(lst(5), c, ptr, len, stride, col, val); break;
-        case 6: c = hc.count[6];
-            k_sort_bucket<512, 8, 1><<<c, 512, 0, t>>>(lst(6), c, ptr, len, stride, col, val); break;
-        case 7: c = hc.count[7];
-            k_sort_bucket<1024, 8, 1><<<c, 1024, 0, t>>>(lst(7), c, ptr, len, stride, col, val); break;
+        case 1: c = hc.count[1]; sort_bucket<64, 1, 4>(lst(1), c, ptr, col, val, t); break;
+        case 2: c = hc.count[2]; sort_bucket<64, 4, 4>(lst(2), c, ptr, col, val, t); break;
+        case 3: c = hc.count[3]; sort_bucket<64, 8, 4>(lst(3), c, ptr, col, val, t); break;
+        case 4: c = hc.count[4]; sort_bucket<128, 8, 1>(lst(4), c, ptr, col, val, t); break;
+        case 5: c = hc.count[5]; sort_bucket<256, 8, 1>(lst(5), c, ptr, col, val, t); break;
+        case 6: c = hc.count[6]; sort_bucket<512, 8, 1>(lst(6), c, ptr, col, val, t); break;
+        case 7: c = hc.count[7]; sort_bucket<1024, 8, 1>(lst(7), c, ptr, col, val, t); break;
         case 8: {
             c = hc.count[8];
             const size_t lds = sortb2_lds((int32_t)plan->n_cols);

@@ -12,6 +12,9 @@ Phases (spgemm_kernels.hpp, Timer marks):
     3 pass 2, 4 pass 3, 5 word prefixes, 6 placement
   sym4 / sym5 (k_sym4, k_sym5): 0 staging, 1 filter, 2 classify, 3 exact,
     4 finish, 5 filter clear
+  sort (k_sort_bucket, --sorted): 0 loads + range, 1 coarse bins, 2 fine
+    buckets, 3 bucket scan, 4 ranks, 5 staging, 6 stores issued;
+    k_sort_bitmap16: 0 loads + clear, 1 bitmap, 2 prefix, 3 ranks, 4 staging + stores
 """
 import argparse
 import ctypes as C
@@ -31,15 +34,17 @@ def main():
     ap.add_argument("--scale", type=int, default=20)
     ap.add_argument("--ef", type=float, default=20)
     ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--sorted", action="store_true", help="IAS_ORDER_SORTED (row sort kernels timed)")
     a = ap.parse_args()
+    order = ias.ORDER_SORTED if a.sorted else ias.ORDER_REFERENCE
     A = ias.gen_rmat(a.scale, a.ef, seed=a.seed)
     f = ias.lib.ias_debug_timing
     f.restype = C.c_int
     f.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     buf = (C.c_ulonglong * (SLOTS * (PH + 1)))()
-    ias.spgemm(A, device=0)          # warm-up
-    f(buf, len(buf))                 # reset
-    _, rep = ias.spgemm(A, device=0)
+    ias.spgemm(A, device=0, order=order)          # warm-up
+    f(buf, len(buf))                               # reset
+    _, rep = ias.spgemm(A, device=0, order=order)
     n = f(buf, len(buf))
     if n <= 0:
         print("not a timing build"); return
@@ -61,6 +66,10 @@ def main():
             kind, team = "sym-part", 1024
         elif slot == 28:
             kind, team = "sym-cbm", 1024
+        elif slot == 17:
+            kind, team = "sortbm16", 1024
+        elif 11 <= slot <= 16:
+            kind, team = "sort", (64 if slot <= 12 else 1 << (slot - 6))
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
         print("%-8s TEAM %4d rows %8d  per-row us: %s  sum %.2f" % (
             kind, team, cnt, " ".join("%6.2f" % u for u in us), sum(us)))
