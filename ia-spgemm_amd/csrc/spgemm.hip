@@ -1784,14 +1784,18 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
             r[k] = s0[k];
             mx = max(mx, sz[k]);
         }
-        // branch-free steps (a clamped read for a finished walk): the E reads
-        // of a step are issued before any compare
+        // lockstep steps: the E reads of a step are issued before any compare;
+        // a finished walk's lanes are masked off its read (the walks are
+        // LDS-bound: a clamped read still took its bank cycles)
         for (uint32_t j = 0; j < mx; ++j) {
             int32_t kj[E];
 #pragma unroll
-            for (int k = 0; k < E; ++k) kj[k] = sk[team][sz[k] ? s0[k] + min(j, sz[k] - 1u) : 0u];
+            for (int k = 0; k < E; ++k) {
+                kj[k] = INT32_MAX;
+                if (j < sz[k]) kj[k] = sk[team][s0[k] + j];
+            }
 #pragma unroll
-            for (int k = 0; k < E; ++k) r[k] += (j < sz[k] && kj[k] < c[k]) ? 1u : 0u;
+            for (int k = 0; k < E; ++k) r[k] += kj[k] < c[k] ? 1u : 0u;
         }
     } else {
         // skewed buckets: the keys alone sorted in LDS (bitonic, padded to a
@@ -1884,20 +1888,25 @@ __global__ __launch_bounds__(1024) void k_sort_global(const RowRef *list, int32_
     }
 }
 
-// Rows beyond the LDS bins: gathered into a compact workspace (their binning
-// slots), sorted there by one segmented radix sort over all of them (every
-// workgroup of the chip works on them, not one per row), scattered back.
-// Sort of a long row by a column bitmap (C's columns are distinct within a
-// row): every entry sets its column's bit in LDS, a prefix of popcounts (per
-// 8 words) gives each column its sorted position, entries land there in the
-// row's slot of a compact workspace and are copied back.  O(n + cols/32) per
-// row against the segmented radix sort's passes over its keys.  Columns below
-// SORTBM_COLS (the bitmap: 128 KB of LDS + 16 KB of prefixes).
+// Rows beyond the LDS bins: sorted by a column bitmap when C has at most
+// SORTBM_COLS columns (C's columns are distinct within a row): every entry
+// sets its column's bit in LDS, a prefix of popcounts (per 8 words) gives
+// each column its sorted position.  O(n + cols/32) per row against a
+// segmented radix sort's passes over its keys.  Bitmap: 128 KB of LDS + 16 KB
+// of prefixes.
 constexpr int SORTBM_T = 1024;
 constexpr int32_t SORTBM_COLS = 1 << 20;
 static_assert(SORTBM_COLS / 256 <= SORTBM_T * 4, "bitmap_prefix8: at most four groups per thread");
+// k_sort_bitmap stages SORTBM_W sorted positions at a time over the dead
+// bitmap (12 B each: 120 KB)
+constexpr int SORTBM_W = 10240;
+constexpr size_t sortbm_area(int32_t cols) {
+    const size_t bm = 4ull * (((size_t)cols + 255) / 256 * 8);
+    const size_t st = 12ull * SORTBM_W;
+    return bm > st ? bm : st;
+}
 constexpr size_t sortbm_lds(int32_t cols) {
-    return 4ull * (((size_t)cols + 255) / 256 * 8) + 4ull * (((size_t)cols + 255) / 256 + 1) + 4ull * 64;
+    return sortbm_area(cols) + 4ull * (((size_t)cols + 255) / 256 + 1) + 4ull * 64;
 }
 // Sorted position of column c from the row's bitmap: the exclusive prefix of
 // its 8-word group plus the popcounts of the group's words below it, the
@@ -1946,20 +1955,30 @@ __device__ __forceinline__ void bitmap_prefix8(const uint32_t *bits, int32_t *pr
     }
 }
 
-// the long rows' passes take SORTBM_B entries per thread at a time, their
-// loads issued together (one global round trip per batch, not per entry)
+// Rows longer than k_sort_bitmap16's (more than fit the registers): a pass
+// sets the bitmap, the next ranks every entry and copies it with its
+// position into the row's slot of a compact workspace (coalesced: the
+// scattered 4- and 8-byte stores of every entry to its sorted slot it
+// replaces took ~96 of a row's 120 us, one cache line per lane), then the
+// sorted row is assembled SORTBM_W positions at a time in LDS over the dead
+// bitmap and written out contiguously in place.  Passes take SORTBM_B
+// entries per thread at a time, their loads issued together.
 constexpr int SORTBM_B = 8;
 __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, int32_t count, const int64_t *ws_off,
-                                                         const int64_t *ptr, const int32_t *len, int64_t stride,
-                                                         int32_t *col, double *val, int32_t ncols, int32_t *wcol,
-                                                         double *wval) {
+                                                         const int64_t *ptr, int32_t *col, double *val,
+                                                         int32_t ncols, int32_t *wcol, double *wval,
+                                                         int32_t *wpos) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sbm[];
     const int NW = (ncols + 255) / 256 * 8;   // bitmap words, a multiple of 8
     uint32_t *bits = sbm;
-    int32_t *pre8 = (int32_t *)(bits + NW);    // exclusive popcount prefix per 8 words
+    int32_t *skey = (int32_t *)sbm;               // staging (after the bitmap is dead)
+    double *sval = (double *)(sbm + SORTBM_W);
+    int32_t *pre8 = (int32_t *)((char *)sbm + sortbm_area(ncols));   // exclusive popcount prefix per 8 words
     int *scratch = pre8 + NW / 8 + 1;
     const int tid = (int)threadIdx.x;
     constexpr int BT = SORTBM_B * SORTBM_T;
+    Timer tm;   // timing builds only (phases: 0 row + clear, 1 bitmap, 2 prefix, 3 ranks + workspace, 4 windows)
+    tm.start();
     for (int64_t idx = blockIdx.x; idx < count; idx += gridDim.x) {
         int64_t o;
         int32_t n;
@@ -1967,6 +1986,7 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, in
         const int64_t w0 = ws_off[idx];
         for (int i = tid; i < NW / 4; i += SORTBM_T) ((uint4 *)bits)[i] = make_uint4(0u, 0u, 0u, 0u);
         __syncthreads();
+        tm.mark(0);
         for (int32_t e0 = 0; e0 < n; e0 += BT) {
             uint32_t c[SORTBM_B];
 #pragma unroll
@@ -1979,8 +1999,10 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, in
                 if (e0 + k * SORTBM_T + tid < n) atomicOr(&bits[c[k] >> 5], 1u << (c[k] & 31));
         }
         __syncthreads();
+        tm.mark(1);
         bitmap_prefix8(bits, pre8, NW, scratch);
         __syncthreads();
+        tm.mark(2);
         for (int32_t e0 = 0; e0 < n; e0 += BT) {
             uint32_t c[SORTBM_B];
             double v[SORTBM_B];
@@ -1991,35 +2013,49 @@ __global__ __launch_bounds__(SORTBM_T) void k_sort_bitmap(const RowRef *list, in
                 v[k] = e < n ? val[o + e] : 0.0;
             }
 #pragma unroll
-            for (int k = 0; k < SORTBM_B; ++k)
-                if (e0 + k * SORTBM_T + tid < n) {
-                    const int pos = bitmap_rank(bits, pre8, c[k]);
-                    wcol[w0 + pos] = (int32_t)c[k];
-                    wval[w0 + pos] = v[k];
-                }
-        }
-        __threadfence_block();
-        __syncthreads();
-        for (int32_t e0 = 0; e0 < n; e0 += BT) {
-            int32_t c[SORTBM_B];
-            double v[SORTBM_B];
-#pragma unroll
-            for (int k = 0; k < SORTBM_B; ++k) {
-                const int32_t e = e0 + k * SORTBM_T + tid;
-                c[k] = e < n ? wcol[w0 + e] : 0;
-                v[k] = e < n ? wval[w0 + e] : 0.0;
-            }
-#pragma unroll
             for (int k = 0; k < SORTBM_B; ++k) {
                 const int32_t e = e0 + k * SORTBM_T + tid;
                 if (e < n) {
-                    col[o + e] = c[k];
-                    val[o + e] = v[k];
+                    wpos[w0 + e] = bitmap_rank(bits, pre8, c[k]);
+                    wcol[w0 + e] = (int32_t)c[k];
+                    wval[w0 + e] = v[k];
                 }
             }
         }
-        __syncthreads();
+        __threadfence_block();
+        __syncthreads();   // the workspace written; the bitmap is dead
+        tm.mark(3);
+        for (int32_t lo = 0; lo < n; lo += SORTBM_W) {
+            const uint32_t m = (uint32_t)min(SORTBM_W, n - lo);
+            for (int32_t e0 = 0; e0 < n; e0 += BT) {
+                uint32_t q[SORTBM_B];
+                int32_t c[SORTBM_B];
+                double v[SORTBM_B];
+#pragma unroll
+                for (int k = 0; k < SORTBM_B; ++k) {
+                    const int32_t e = e0 + k * SORTBM_T + tid;
+                    q[k] = e < n ? (uint32_t)(wpos[w0 + e] - lo) : ~0u;
+                    c[k] = e < n ? wcol[w0 + e] : 0;
+                    v[k] = e < n ? wval[w0 + e] : 0.0;
+                }
+#pragma unroll
+                for (int k = 0; k < SORTBM_B; ++k)
+                    if (q[k] < m) {
+                        skey[q[k]] = c[k];
+                        sval[q[k]] = v[k];
+                    }
+            }
+            __syncthreads();
+            for (uint32_t e = tid; e < m; e += SORTBM_T) {
+                col[o + lo + e] = skey[e];
+                val[o + lo + e] = sval[e];
+            }
+            __syncthreads();
+        }
+        tm.mark(4);
+        tm.done();
     }
+    tm.flush(18, tid == 0);
 }
 
 // Rows of 8,193 .. 16,384 entries (C has at most SORTBM_COLS columns): the
@@ -3561,7 +3597,7 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
     // wide rows by the column bitmap when C's columns fit it (the compact
     // workspace of the radix path, 12 B per entry, is its staging)
     const bool bitmap_sort = nwide > 0 && !force_global && plan->n_cols > 0 && plan->n_cols <= SORTBM_COLS;
-    if (bitmap_sort && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * slots + 16ull * nwide + 256));
+    if (bitmap_sort && !radix) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 16ull * slots + 16ull * nwide + 256));
     if (nwide > 0 && !radix && !bitmap_sort) IAS_TRY(plan->reserve(ias_plan::B_TMP4, 12ull * hc.ws_slots + 16));
     // one wave per row up to 512 entries (4 rows per workgroup, wave
     // barriers only), then teams sized so a row fills ~half their slots.
@@ -3593,14 +3629,15 @@ static ias_status sort_rows_impl(ias_plan *plan, const int64_t *ptr, const int32
             c = nwide;
             if (bitmap_sort) {
                 char *bp = (char *)plan->bufs[ias_plan::B_TMP4].p;
-                double *wv = (double *)bp;
+                double *wv = (double *)bp;   // 16 B per slot: value, column, position
                 int32_t *wc = (int32_t *)(wv + slots);
+                int32_t *wp = wc + slots;
                 const size_t lds = sortbm_lds((int32_t)plan->n_cols);
                 static bool sb_done = false;
                 allow_lds(k_sort_bitmap, sb_done, lds);
                 const int64_t grid = std::min<int64_t>(c, resident_blocks(k_sort_bitmap, SORTBM_T, lds));
                 k_sort_bitmap<<<(unsigned)std::max<int64_t>(grid, 1), SORTBM_T, lds, t>>>(
-                    lst(wide), c, coff, ptr, len, stride, col, val, (int32_t)plan->n_cols, wc, wv);
+                    lst(wide), c, coff, ptr, col, val, (int32_t)plan->n_cols, wc, wv, wp);
             } else if (radix) {
                 char *bp = (char *)plan->bufs[ias_plan::B_TMP4].p;
                 double *vin = (double *)bp;

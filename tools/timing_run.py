@@ -14,7 +14,8 @@ Phases (spgemm_kernels.hpp, Timer marks):
     4 finish, 5 filter clear
   sort (k_sort_bucket, --sorted): 0 loads + range, 1 coarse bins, 2 fine
     buckets, 3 bucket scan, 4 ranks, 5 staging, 6 stores issued;
-    k_sort_bitmap16: 0 loads + clear, 1 bitmap, 2 prefix, 3 ranks, 4 staging + stores
+    k_sort_bitmap16: 0 loads + clear, 1 bitmap, 2 prefix, 3 ranks, 4 staging + stores;
+    k_sort_bitmap: 0 row + clear, 1 bitmap, 2 prefix, 3 ranks + workspace, 4 copy back
 """
 import argparse
 import ctypes as C
@@ -68,6 +69,8 @@ def main():
             kind, team = "sym-cbm", 1024
         elif slot == 17:
             kind, team = "sortbm16", 1024
+        elif slot == 18:
+            kind, team = "sortbm", 1024
         elif 11 <= slot <= 16:
             kind, team = "sort", (64 if slot <= 12 else 1 << (slot - 6))
         us = [row[i] / cnt / 100.0 for i in range(PH)]   # wall clock: 100 MHz
