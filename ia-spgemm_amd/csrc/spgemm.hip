@@ -1768,10 +1768,7 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
     }
     uint32_t r[E];
     if (!heavy) {
-#pragma unroll
-        for (int k = 0; k < E; ++k)
-            if (k * TEAM + lane < n) sk[team][hist[b[k]] + pib[k]] = c[k];
-        lds_sync<TM::MULTI>();
+        // each bucket's start and size read once: for the key's slot and its walk
         uint32_t s0[E], sz[E], mx = 0u;
 #pragma unroll
         for (int k = 0; k < E; ++k) {
@@ -1780,10 +1777,12 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
             if (k * TEAM + lane < n) {
                 s0[k] = hist[b[k]];
                 sz[k] = hist[b[k] + 1] - s0[k];
+                sk[team][s0[k] + pib[k]] = c[k];
             }
             r[k] = s0[k];
             mx = max(mx, sz[k]);
         }
+        lds_sync<TM::MULTI>();
         // lockstep steps: the E reads of a step are issued before any compare;
         // a finished walk's lanes are masked off its read (the walks are
         // LDS-bound: a clamped read still took its bank cycles)
