@@ -1561,6 +1561,8 @@ __device__ __forceinline__ void sort_row_span(const int64_t *ptr, const int32_t 
     }
 }
 
+__host__ __device__ constexpr int sort_pow2_floor(int x) { return x < 2 ? 1 : 2 * sort_pow2_floor(x / 2); }
+
 // A team barrier for LDS only: waits for this wave's LDS operations, not for
 // its global loads in flight (a workgroup fence waits for both, which would
 // stall the sort's prefetch at the next barrier).  The "memory" clobber keeps
@@ -1602,9 +1604,12 @@ __global__ __launch_bounds__(TEAM *TPW) void k_sort_bucket(const RowRef *list, i
     constexpr int CAP = TEAM * E;
     constexpr int NBM = TEAM < 1024 ? CAP : CAP / 2;        // most buckets
     constexpr int NBT = (NBM + TEAM - 1) / TEAM;            // bucket counts per thread in the scan
-    constexpr int G = CAP / 2 < 2 ? 1 : (CAP / 2 < 256 ? CAP / 2 : 256);   // coarse bins
-    constexpr int GT = (G + TEAM - 1) / TEAM;
     constexpr int SVC = TEAM < 1024 ? CAP : CAP / 2;        // values staged per round
+    // coarse bins: as many as fit beside the bucket counts in the staging
+    // area, at most 1,024 (finer bins equalise better: modelled on K3''s
+    // rows, 256 -> 1,024 bins takes the walks 10.3 -> 8.4 steps per wave)
+    constexpr int G = sort_pow2_floor((2 * SVC - NBM - 2) < 1024 ? (2 * SVC - NBM - 2) : 1024);
+    constexpr int GT = (G + TEAM - 1) / TEAM;
     static_assert(2 * SVC >= NBM + G + 2, "the bucket counts and the coarse bins overlay the value staging");
     __shared__ int32_t sk[TPW][CAP];
     __shared__ double sv[TPW][SVC];
